@@ -1,0 +1,224 @@
+/*
+ * sglm.h -- C ABI of the MI355X fitting engine for sparkGLM's lm()/glm() hot path.
+ *
+ * This is the drop-in boundary.  The reference (cafreeman/sparkGLM, Scala/Spark) has no
+ * FFI of its own; the seam is internal: the fit drivers return PreGLM / PreLM and the
+ * unchanged model code (GLM.createObj, new LM) builds the user-visible objects.  Each
+ * entry point below replaces one reference function body, reached from Scala over JNI
+ * (binding stubs in INTEGRATION.md):
+ *
+ *   sglm_set_data        replaces utils.dataFrameToMatrix / dfToDenseMatrix
+ *                        (utils.scala:36-49) + the per-action re-conversion: one upload,
+ *                        X stays resident in HBM across iterations and fits.
+ *   sglm_fit_glm         replaces GLM.fitSingleBinomial (GLM.scala:254-315) and
+ *                        GLM.fitMultipleBinomial (GLM.scala:410-468); output = PreGLM
+ *                        (GLM.scala:25-33).
+ *   sglm_fit_lm          replaces LM.fitSingle / LM.fitMultiple (LM.scala:191-237) and
+ *                        the stderr tail of LM.fit (LM.scala:260-263); output = PreLM
+ *                        (LM.scala:10-14) + stdErr/sigma.
+ *   sglm_irls_pass       one IRLS pass (zwCreateBinomial + wlsComponents, GLM.scala:
+ *                        359-395, utils.scala:110-126) for tests and benchmarks.
+ *   sglm_predict         replaces LM.predictSingle/predictMultiple's newX * coefs
+ *                        (LM.scala:39-61).
+ *   sglm_glm_summary / sglm_lm_summary
+ *                        the printed summaries of GLM.summary (GLM.scala:998-1025) and
+ *                        SummaryLM (LM.scala:66-137), produced host-side in C++.
+ *
+ * Conventions
+ *   - Status codes: 0 ok; SGLM_EINVAL maps to IllegalArgumentException (the reference's
+ *     require(...)); SGLM_ESINGULAR to breeze MatrixSingularException; SGLM_EHIP /
+ *     SGLM_ECOMM to RuntimeException.  sglm_last_error() returns a thread-local message.
+ *   - Matrices are column-major fp64 (Breeze DenseMatrix layout): element (i,j) at
+ *     X[i + j*ldx].  The caller keeps ownership of every pointer it passes; the engine
+ *     copies into device memory it owns until sglm_destroy.
+ *   - One engine handle drives one HIP device.  Multi-GPU = one process (or thread) per
+ *     device, each holding its row shard, joined by a communicator (RCCL over xGMI, or a
+ *     caller-supplied all-reduce).  Every rank receives identical results.
+ *   - Handles are not thread-safe; distinct handles may be used concurrently.
+ */
+#ifndef SGLM_H
+#define SGLM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGLM_ABI_VERSION 1
+
+enum sglm_status {
+  SGLM_OK = 0,
+  SGLM_EINVAL = 1,    /* require(...) failed -> IllegalArgumentException */
+  SGLM_ESINGULAR = 2, /* inv() of a singular matrix -> MatrixSingularException */
+  SGLM_EHIP = 3,      /* HIP runtime / device error */
+  SGLM_ECOMM = 4,     /* RCCL or caller all-reduce failure */
+  SGLM_ENOMEM = 5     /* device or host allocation failed */
+};
+
+/* Families: the reference fits only binomial (GLM.scala:486-590); the rest follow R's
+ * family objects on the reference's IRLS skeleton. */
+enum sglm_family { SGLM_BINOMIAL = 0, SGLM_GAUSSIAN = 1, SGLM_POISSON = 2, SGLM_GAMMA = 3 };
+enum sglm_link {
+  SGLM_LOGIT = 0, SGLM_PROBIT = 1, SGLM_CLOGLOG = 2, /* binomial (GLM.scala:190-251) */
+  SGLM_IDENTITY = 3, SGLM_LOG = 4, SGLM_INVERSE = 5   /* gaussian / poisson / gamma */
+};
+
+/* How mu is formed on the first iteration. */
+enum sglm_init {
+  SGLM_INIT_SINGLE = 0,  /* fitSingleBinomial: mu = mean(y) directly (GLM.scala:263, 282-290) */
+  SGLM_INIT_MULTIPLE = 1 /* fitMultipleBinomial: mu = unlink(link(mean(y))) (GLM.scala:370-371) */
+};
+
+typedef struct sglm_engine sglm_engine;
+
+typedef struct {
+  int family;      /* enum sglm_family */
+  int link;        /* enum sglm_link */
+  double tol;      /* absolute |delta deviance| stopping tolerance; reference default 1e-6 */
+  int verbose;     /* print "iter\tdeltad" per iteration (GLM.scala:304, 461) */
+  int max_iter;    /* 0 = unbounded, as in the reference (extension guard otherwise) */
+  int init_mode;   /* enum sglm_init */
+  int npart;       /* value reported in PreGLM.npart (reference: Spark partition count); 0 = #ranks */
+} sglm_glm_opts;
+
+typedef struct { /* PreGLM (GLM.scala:25-33) */
+  double *coefs;        /* [p] caller-allocated */
+  double *std_err;      /* [p] caller-allocated: sqrt(diag(inv(X'WX))) of the last solve */
+  double deviance;
+  double null_deviance;
+  double pearson;
+  double loglik;
+  int iter;
+  double nrow;
+  int npart;
+  double *dev_trace;    /* optional [max_trace]: deviance after each iteration, [0] = null */
+  int max_trace;
+} sglm_preglm;
+
+typedef struct { /* PreLM (LM.scala:10-14) + LM.fit's derived stdErr / sigma */
+  double *coefs;        /* [p] */
+  double *xtxi;         /* [p*p] col-major inv(X'X), may be NULL */
+  double *std_err;      /* [p] sqrt(sse/(n-p) * diag(xtxi)) (LM.scala:260-263) */
+  double sse;
+  double r2;            /* SSR/SST, as the reference (LM.scala:185) */
+  double fstat;
+  double sigma;
+  double nrow;
+  int npart;
+} sglm_prelm;
+
+/* Per-handle timing counters (HIP events on the engine stream). */
+typedef struct {
+  int64_t passes;           /* fused IRLS / LM passes launched */
+  double pass_kernel_ms;    /* total time of the fused pass kernel (sum over passes) */
+  double reduce_kernel_ms;  /* total time of the partial-reduction kernel */
+  double last_pass_ms;      /* fused kernel time of the last pass */
+  double comm_ms;           /* host wall time in the all-reduce */
+  double solve_ms;          /* host wall time in the p x p solves */
+  int64_t n_local;          /* rows resident on this device */
+  int64_t p;
+  int workgroups;           /* fused-kernel grid size */
+  int kernel_variant;       /* column-block count P16 of the instantiated kernel */
+} sglm_stats;
+
+/* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
+ * pointer and stream the engine's hipStream_t; otherwise buf is host memory. */
+typedef int (*sglm_allreduce_fn)(void *ctx, double *buf, int64_t count, void *stream, int on_device);
+
+/* ---- lifecycle ---------------------------------------------------------------- */
+int sglm_abi_version(void);
+const char *sglm_last_error(void);
+int sglm_device_count(int *count);
+int sglm_create(int device, sglm_engine **out);
+void sglm_destroy(sglm_engine *h);
+
+/* ---- data (utils.dataFrameToMatrix replacement) ------------------------------ */
+/* Host arrays.  m (binomial trials), offset and prior (weights) may be NULL. */
+int sglm_set_data(sglm_engine *h, const double *X, int64_t n, int64_t p, int64_t ldx,
+                  const double *y, const double *m, const double *offset, const double *prior);
+/* Same, from device memory already on this engine's device. */
+int sglm_set_data_device(sglm_engine *h, const double *dX, int64_t n, int64_t p, int64_t ldx,
+                         const double *dy, const double *dm, const double *doffset,
+                         const double *dprior);
+/* Generate this rank's row shard [row0, row0+n) of the seeded synthetic design directly
+ * in HBM (bench / scale tests).  kind: 0 = logit design (y in {0,1}), 1 = gaussian (LM),
+ * 2 = poisson counts + offset + prior.  Column 0 is the intercept.  Bit-identical to
+ * sparkglm_amd.synth on the host. */
+int sglm_synth(sglm_engine *h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed);
+/* Copy back the resident design (tests; X col-major with ldx = n). */
+int sglm_get_data(sglm_engine *h, double *X, double *y, double *m, double *offset, double *prior);
+
+/* ---- communicators (Spark treeReduce replacement) ----------------------------- */
+int sglm_set_comm(sglm_engine *h, sglm_allreduce_fn fn, void *ctx, int on_device);
+/* Native RCCL communicator over xGMI.  unique_id: 128 bytes from
+ * sglm_rccl_unique_id() on rank 0, broadcast by the caller. */
+int sglm_rccl_unique_id(void *out128);
+int sglm_set_comm_rccl(sglm_engine *h, int nranks, int rank, const void *unique_id128);
+
+/* ---- fits ---------------------------------------------------------------------- */
+int sglm_fit_glm(sglm_engine *h, const sglm_glm_opts *opts, sglm_preglm *out);
+int sglm_fit_lm(sglm_engine *h, sglm_prelm *out);
+
+/* One IRLS pass at beta (beta == NULL: the initial constant-eta pass at mu0),
+ * all-reduced over the communicator.  Outputs (any may be NULL): gram [p*p] col-major
+ * full symmetric X'WX, xtwz [p], scalars [8] = {deviance-sum, pearson, loglik-part, bad,
+ * aux0, aux1, aux2, sum prior}. */
+int sglm_irls_pass(sglm_engine *h, const sglm_glm_opts *opts, const double *beta, double mu0,
+                   double *gram, double *xtwz, double *scalars);
+
+/* `iters` IRLS iterations from beta (in/out): each is one fused pass at beta followed by
+ * the p x p solve -- the unit the benchmark times.  last_dev (may be NULL) receives the
+ * deviance at the last input beta. */
+int sglm_irls_iterations(sglm_engine *h, const sglm_glm_opts *opts, double *beta, int iters,
+                         double *last_dev);
+
+/* eta = X * beta (+ offset if add_offset) for the resident rows, written to out [n_local]. */
+int sglm_predict(sglm_engine *h, const double *beta, int add_offset, double *out);
+
+int sglm_get_stats(sglm_engine *h, sglm_stats *out);
+int sglm_reset_stats(sglm_engine *h);
+
+/* ---- external backend: the same IRLS driver over caller-computed partials ---------
+ * Lets a host (or a test) run the engine's driver, solve and convergence logic over
+ * partial sums produced elsewhere (e.g. a CPU shard).  pass() must write the packed
+ * wire format: lower-triangular X'WX row-major (i>=j: i*(i+1)/2+j), then X'Wz [p], then
+ * 8 scalars.  mode: 0 irls(beta), 1 init-single, 2 init-multiple, 3 lm-gram, 4 lm-resid. */
+typedef struct {
+  void *ctx;
+  int64_t p;
+  int (*local_sums)(void *ctx, double *out2 /* {sum y, n_local} */);
+  int (*pass)(void *ctx, int mode, const double *beta, double mu0, double ybar, double *packed);
+} sglm_backend;
+
+int sglm_fit_glm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *comm_ctx,
+                          const sglm_glm_opts *opts, sglm_preglm *out);
+int sglm_fit_lm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *comm_ctx,
+                         sglm_prelm *out);
+
+/* ---- model objects and printed summaries (host-side, C++) ---------------------- */
+/* GLM.createObj (GLM.scala:59-88) derived fields. */
+typedef struct {
+  double df_residual, df_null, p_dispersion, aic;
+} sglm_glm_derived;
+int sglm_glm_create_obj(const sglm_preglm *pre, int64_t p, sglm_glm_derived *out);
+/* GLM.summary text (GLM.scala:998-1025). xnames: p C strings. Returns bytes needed. */
+int64_t sglm_glm_summary(const sglm_preglm *pre, int64_t p, const char *const *xnames,
+                         const char *yname, const char *family, const char *link, char *buf,
+                         int64_t buflen);
+/* SummaryLM.print text (LM.scala:128-136). */
+int64_t sglm_lm_summary(const sglm_prelm *pre, int64_t p, const char *const *xnames,
+                        const char *yname, char *buf, int64_t buflen);
+/* Helpers reproduced from utils.scala:146-169 and java.lang.Double.toString. */
+double sglm_sig_digits(double num, int digits);
+double sglm_round_digits(double num, int digits);
+int64_t sglm_java_double_string(double x, char *buf, int64_t buflen);
+/* 2*(1-Phi(|z|)) and 2*(1-T_df(|t|)) as used by the summaries. */
+double sglm_pval_normal(double z);
+double sglm_pval_t(double t, double df);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGLM_H */

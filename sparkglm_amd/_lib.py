@@ -1,0 +1,168 @@
+"""ctypes binding of libsglm_hip.so (the C ABI declared in include/sglm.h).
+
+The library is built in-tree (sparkglm_amd/lib/) by ``python -m sparkglm_amd.build`` or
+``__graft_entry__.build()``.  There is no fallback: if the HIP library is missing the
+import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsglm_hip.so")
+
+SGLM_OK, SGLM_EINVAL, SGLM_ESINGULAR, SGLM_EHIP, SGLM_ECOMM, SGLM_ENOMEM = range(6)
+FAMILIES = {"binomial": 0, "gaussian": 1, "poisson": 2, "gamma": 3}
+LINKS = {"logit": 0, "probit": 1, "cloglog": 2, "identity": 3, "log": 4, "inverse": 5}
+CANONICAL_LINK = {"gaussian": "identity", "poisson": "log", "gamma": "inverse"}
+INIT_SINGLE, INIT_MULTIPLE = 0, 1
+NS = 8
+S_DEV, S_PEARSON, S_LL, S_BAD, S_AUX0, S_AUX1, S_AUX2, S_SUMW = range(8)
+
+# Symbols include/sglm.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "sglm_abi_version", "sglm_last_error", "sglm_device_count", "sglm_create", "sglm_destroy",
+    "sglm_set_data", "sglm_set_data_device", "sglm_synth", "sglm_get_data", "sglm_set_comm",
+    "sglm_rccl_unique_id", "sglm_set_comm_rccl", "sglm_fit_glm", "sglm_fit_lm", "sglm_irls_pass",
+    "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
+    "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
+    "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
+    "sglm_pval_normal", "sglm_pval_t",
+]
+
+dp = C.POINTER(C.c_double)
+
+
+class GlmOpts(C.Structure):
+    _fields_ = [("family", C.c_int), ("link", C.c_int), ("tol", C.c_double), ("verbose", C.c_int),
+                ("max_iter", C.c_int), ("init_mode", C.c_int), ("npart", C.c_int)]
+
+
+class PreGLM(C.Structure):
+    _fields_ = [("coefs", dp), ("std_err", dp), ("deviance", C.c_double), ("null_deviance", C.c_double),
+                ("pearson", C.c_double), ("loglik", C.c_double), ("iter", C.c_int), ("nrow", C.c_double),
+                ("npart", C.c_int), ("dev_trace", dp), ("max_trace", C.c_int)]
+
+
+class PreLM(C.Structure):
+    _fields_ = [("coefs", dp), ("xtxi", dp), ("std_err", dp), ("sse", C.c_double), ("r2", C.c_double),
+                ("fstat", C.c_double), ("sigma", C.c_double), ("nrow", C.c_double), ("npart", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("passes", C.c_int64), ("pass_kernel_ms", C.c_double), ("reduce_kernel_ms", C.c_double),
+                ("last_pass_ms", C.c_double), ("comm_ms", C.c_double), ("solve_ms", C.c_double),
+                ("n_local", C.c_int64), ("p", C.c_int64), ("workgroups", C.c_int), ("kernel_variant", C.c_int)]
+
+
+class GlmDerived(C.Structure):
+    _fields_ = [("df_residual", C.c_double), ("df_null", C.c_double), ("p_dispersion", C.c_double),
+                ("aic", C.c_double)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, dp, C.c_int64, C.c_void_p, C.c_int)
+LOCAL_SUMS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, dp)
+PASS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, dp, C.c_double, C.c_double, dp)
+
+
+class Backend(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("p", C.c_int64), ("local_sums", LOCAL_SUMS_FN), ("pass_", PASS_FN)]
+
+
+class SGLMError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[sglm status {code}] {msg}")
+        self.code = code
+
+
+class IllegalArgumentException(ValueError):
+    """The reference's require(...) failures (java.lang.IllegalArgumentException)."""
+
+
+class MatrixSingularException(ArithmeticError):
+    """breeze.linalg.MatrixSingularException raised by inv()."""
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"sparkglm_amd: HIP engine library missing at {LIB_PATH}; "
+                          f"build it with `python -m sparkglm_amd.build`")
+    lib = C.CDLL(LIB_PATH)
+    E = C.POINTER(C.c_void_p)
+    h = C.c_void_p
+    sig = {
+        "sglm_abi_version": ([], C.c_int),
+        "sglm_last_error": ([], C.c_char_p),
+        "sglm_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "sglm_create": ([C.c_int, E], C.c_int),
+        "sglm_destroy": ([h], None),
+        "sglm_set_data": ([h, dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, dp], C.c_int),
+        "sglm_set_data_device": ([h, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p], C.c_int),
+        "sglm_synth": ([h, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64], C.c_int),
+        "sglm_get_data": ([h, dp, dp, dp, dp, dp], C.c_int),
+        "sglm_set_comm": ([h, ALLREDUCE_FN, C.c_void_p, C.c_int], C.c_int),
+        "sglm_rccl_unique_id": ([C.c_void_p], C.c_int),
+        "sglm_set_comm_rccl": ([h, C.c_int, C.c_int, C.c_void_p], C.c_int),
+        "sglm_fit_glm": ([h, C.POINTER(GlmOpts), C.POINTER(PreGLM)], C.c_int),
+        "sglm_fit_lm": ([h, C.POINTER(PreLM)], C.c_int),
+        "sglm_irls_pass": ([h, C.POINTER(GlmOpts), dp, C.c_double, dp, dp, dp], C.c_int),
+        "sglm_irls_iterations": ([h, C.POINTER(GlmOpts), dp, C.c_int, dp], C.c_int),
+        "sglm_predict": ([h, dp, C.c_int, dp], C.c_int),
+        "sglm_get_stats": ([h, C.POINTER(Stats)], C.c_int),
+        "sglm_reset_stats": ([h], C.c_int),
+        "sglm_fit_glm_external": ([C.POINTER(Backend), ALLREDUCE_FN, C.c_void_p, C.POINTER(GlmOpts),
+                                   C.POINTER(PreGLM)], C.c_int),
+        "sglm_fit_lm_external": ([C.POINTER(Backend), ALLREDUCE_FN, C.c_void_p, C.POINTER(PreLM)], C.c_int),
+        "sglm_glm_create_obj": ([C.POINTER(PreGLM), C.c_int64, C.POINTER(GlmDerived)], C.c_int),
+        "sglm_glm_summary": ([C.POINTER(PreGLM), C.c_int64, C.POINTER(C.c_char_p), C.c_char_p, C.c_char_p,
+                              C.c_char_p, C.c_char_p, C.c_int64], C.c_int64),
+        "sglm_lm_summary": ([C.POINTER(PreLM), C.c_int64, C.POINTER(C.c_char_p), C.c_char_p, C.c_char_p,
+                             C.c_int64], C.c_int64),
+        "sglm_sig_digits": ([C.c_double, C.c_int], C.c_double),
+        "sglm_round_digits": ([C.c_double, C.c_int], C.c_double),
+        "sglm_java_double_string": ([C.c_double, C.c_char_p, C.c_int64], C.c_int64),
+        "sglm_pval_normal": ([C.c_double], C.c_double),
+        "sglm_pval_t": ([C.c_double, C.c_double], C.c_double),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return (load().sglm_last_error() or b"").decode()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == SGLM_OK:
+        return
+    msg = last_error()
+    if rc == SGLM_EINVAL:
+        raise IllegalArgumentException(msg)
+    if rc == SGLM_ESINGULAR:
+        raise MatrixSingularException(msg)
+    raise SGLMError(rc, f"{what}: {msg}" if what else msg)
+
+
+def ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(dp)
+
+
+def java_double_str(x: float) -> str:
+    buf = C.create_string_buffer(64)
+    load().sglm_java_double_string(float(x), buf, 64)
+    return buf.value.decode()

@@ -1,0 +1,63 @@
+// common.hpp -- shared definitions for the sparkGLM MI355X engine (host + device).
+#pragma once
+#include <cstdint>
+
+namespace sglm {
+
+// Rows per LDS row block of the fused pass (one DMA'd tile of X).
+constexpr int RB = 32;
+// Scalar slots appended to every packed partial / reduced buffer.
+constexpr int NS = 8;
+enum Scalar : int { S_DEV = 0, S_PEARSON = 1, S_LL = 2, S_BAD = 3, S_AUX0 = 4, S_AUX1 = 5, S_AUX2 = 6, S_SUMW = 7 };
+
+// Pass modes (shared with sglm_backend.pass in include/sglm.h).
+enum PassMode : int {
+  MODE_IRLS = 0,        // eta = X beta + offset (etaCreate, GLM.scala:321-332)
+  MODE_INIT_SINGLE = 1, // eta = link(mu0, m), mu = mu0            (GLM.scala:263-270)
+  MODE_INIT_MULTI = 2,  // eta = link(mu0, m), mu = unlink(eta, m) (GLM.scala:429-442, 370)
+  MODE_LM_GRAM = 3,     // w = 1, z = y: X'X and X'y (LM.scala:142-155)
+  MODE_LM_RESID = 4     // no Gram: SSE/SSR/SST at beta (LM.scala:160-188)
+};
+
+enum Family : int { FAM_BINOMIAL = 0, FAM_GAUSSIAN = 1, FAM_POISSON = 2, FAM_GAMMA = 3 };
+enum Link : int { LNK_LOGIT = 0, LNK_PROBIT = 1, LNK_CLOGLOG = 2, LNK_IDENTITY = 3, LNK_LOG = 4, LNK_INVERSE = 5 };
+
+// Largest column-block count of the fused (single-panel) kernel: p <= 16*16 = 256.
+constexpr int MAX_P16 = 16;
+
+inline int64_t tri_count(int64_t p) { return p * (p + 1) / 2; }
+inline int64_t packed_len(int64_t p) { return tri_count(p) + p + NS; }
+
+// Arguments of one fused pass launch.
+struct PassArgs {
+  const double* X;      // col-major, leading dimension ld, p columns
+  int64_t ld;
+  int p;
+  const double* y;
+  const double* m;      // may be null (binomial trials = 1)
+  const double* off;    // may be null
+  const double* prior;  // may be null
+  const double* beta;   // device, >= p entries (MODE_IRLS / MODE_LM_RESID)
+  int64_t n;            // valid rows
+  int64_t nblocks;      // row blocks of RB rows (ld == nblocks*RB)
+  int family, link, mode;
+  double mu0;           // init modes
+  double ybar;          // LM resid mode
+  double* partials;     // [grid][stride]
+  int64_t stride;
+  double* eta_out;      // optional [n]: eta of MODE_IRLS rows (for the final statistics)
+};
+
+// Arguments of the final-statistics pass (stats_kernel).
+struct StatsArgs {
+  const double* y;
+  const double* m;
+  const double* prior;
+  const double* eta;    // MODE_IRLS: eta of the last pass; MODE_LM_RESID: X*coefs
+  int64_t n;
+  int family, link, mode;
+  double mu0, ybar;
+  double* partials;     // [grid][NS]
+};
+
+}  // namespace sglm

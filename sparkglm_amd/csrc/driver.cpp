@@ -1,0 +1,211 @@
+// driver.cpp -- the IRLS (Fisher scoring) and least-squares drivers.
+//
+// glm_drive restates the loop of GLM.fitSingleBinomial (GLM.scala:254-315) and
+// GLM.fitMultipleBinomial (GLM.scala:410-468) over any Backend:
+//   mu0 = mean(y); eta0 = link(mu0) with the offset ignored; dev0 = nullDeviance
+//   while |dev_k - dev_{k-1}| > tol (absolute; deltad starts at 1.0):
+//       beta = solve(X'WX, X'Wz)          (wlsSingle / wlsMultiple)
+//       eta = X beta + offset; mu = unlink(eta); dev = deviance(mu)   (one fused pass)
+//   stdErr = sqrt(diag(inv(X'WX))) of the last solve; pearson / loglik at the final mu.
+// Each backend pass returns the NEXT iteration's X'WX together with the current deviance,
+// so one pass over X serves both halves of a reference iteration.
+#include "driver.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "solve.hpp"
+
+extern "C" int64_t sglm_java_double_string(double x, char* buf, int64_t buflen);
+
+namespace sglm {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* get_error() { return g_err.c_str(); }
+
+int family_link_valid(int family, int link) {
+  switch (family) {
+    case FAM_BINOMIAL: return link == LNK_LOGIT || link == LNK_PROBIT || link == LNK_CLOGLOG;
+    case FAM_GAUSSIAN: return link == LNK_IDENTITY;
+    case FAM_POISSON: return link == LNK_LOG;
+    case FAM_GAMMA: return link == LNK_INVERSE;
+    default: return 0;
+  }
+}
+
+double family_dev_factor(int family) { return family == FAM_GAUSSIAN ? 1.0 : 2.0; }
+
+void unpack_gram(const double* packed, int64_t p, double* gram, double* xtwz) {
+  for (int64_t i = 0; i < p; ++i)
+    for (int64_t j = 0; j <= i; ++j) {
+      const double v = packed[i * (i + 1) / 2 + j];
+      gram[i + j * p] = v;
+      gram[j + i * p] = v;
+    }
+  std::memcpy(xtwz, packed + tri_count(p), sizeof(double) * (size_t)p);
+}
+
+static double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// Loglik from the final-statistics scalars (families without per-row closed forms).
+static double family_loglik(int family, const double* s, double dev, double nrow) {
+  if (family == FAM_GAUSSIAN) {
+    // R gaussian()$aic with sigma^2 = dev/n: -(n/2)(log(2 pi dev/n) + 1) + 0.5 sum(log w)
+    return -(nrow / 2.0) * (std::log(2.0 * M_PI * dev / nrow) + 1.0) + 0.5 * s[S_LL];
+  }
+  if (family == FAM_GAMMA) {
+    // R Gamma()$aic: disp = dev / sum(w); sum w * dgamma(y, 1/disp, scale = mu*disp, log)
+    const double sw = s[S_SUMW], disp = dev / sw, a = 1.0 / disp;
+    return (a - 1.0) * s[S_LL] - s[S_AUX0] / disp - (std::lgamma(a) + a * std::log(disp)) * sw - a * s[S_AUX1];
+  }
+  return s[S_LL];
+}
+
+int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
+  if (!family_link_valid(o.family, o.link)) {
+    set_error("requirement failed: unsupported family/link combination");
+    return SGLM_EINVAL;
+  }
+  const int64_t p = be.ncols();
+  const size_t pk = (size_t)packed_len(p);
+  std::vector<double> packed(pk), gram((size_t)(p * p)), xtwz((size_t)p), beta((size_t)p, 0.0), s(NS);
+  Solver solver(p);
+  double sums[2];
+  int rc = be.global_sums(sums);
+  if (rc) return rc;
+  const double nrow = sums[1];
+  if (!(nrow > 0)) {
+    set_error("requirement failed: The number of rows must be strictly greater than 0");
+    return SGLM_EINVAL;
+  }
+  const double ymean = sums[0] / nrow;  // GLM.scala:263 / 423
+  const double fac = family_dev_factor(o.family);
+  const int init_mode = (o.init_mode == SGLM_INIT_MULTIPLE) ? MODE_INIT_MULTI : MODE_INIT_SINGLE;
+
+  rc = be.pass(init_mode, nullptr, ymean, 0.0, o.family, o.link, packed.data());
+  if (rc) return rc;
+  double dev = fac * packed[tri_count(p) + p + S_DEV];
+  const double null_dev = dev;  // GLM.scala:272 / 444
+  double deltad = 1.0;
+  int iter = 0;
+  if (out->dev_trace && out->max_trace > 0) out->dev_trace[0] = dev;
+
+  while (std::fabs(deltad) > o.tol) {  // GLM.scala:281 / 452
+    if (o.max_iter > 0 && iter >= o.max_iter) break;
+    unpack_gram(packed.data(), p, gram.data(), xtwz.data());
+    const double t0 = now_ms();
+    const int srv = solver.solve(gram.data(), xtwz.data(), beta.data());
+    be.solve_ms += now_ms() - t0;
+    if (srv) {
+      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return SGLM_ESINGULAR;
+    }
+    rc = be.pass(MODE_IRLS, beta.data(), ymean, 0.0, o.family, o.link, packed.data());
+    if (rc) return rc;
+    const double dev_old = dev;
+    dev = fac * packed[tri_count(p) + p + S_DEV];
+    deltad = dev - dev_old;
+    iter = iter + 1;
+    if (out->dev_trace && iter < out->max_trace) out->dev_trace[iter] = dev;
+    if (o.verbose) {  // println(iter.toString + "\t" + deltad.toString)  (GLM.scala:304)
+      char buf[64];
+      sglm_java_double_string(deltad, buf, sizeof buf);
+      std::printf("%d\t%s\n", iter, buf);
+      std::fflush(stdout);
+    }
+  }
+
+  rc = be.stats(iter > 0 ? MODE_IRLS : init_mode, beta.data(), ymean, 0.0, o.family, o.link, s.data());
+  if (rc) return rc;
+  if (s[S_BAD] > 0) {
+    set_error("requirement failed: Binomial(m.toInt, mu).logProbabilityOf(y.toInt) needs 0 <= y <= m, m >= 1");
+    return SGLM_EINVAL;
+  }
+  std::vector<double> d((size_t)p, 0.0);
+  solver.inv_diag(d.data());
+  for (int64_t i = 0; i < p; ++i) {
+    out->coefs[i] = beta[i];
+    out->std_err[i] = std::sqrt(d[i]);  // GLM.scala:307 / 464 (utils.scala:105)
+  }
+  out->deviance = dev;
+  out->null_deviance = null_dev;
+  out->pearson = s[S_PEARSON];
+  out->loglik = family_loglik(o.family, s.data(), dev, nrow);
+  out->iter = iter;
+  out->nrow = nrow;
+  out->npart = o.npart > 0 ? o.npart : be.npart();
+  return SGLM_OK;
+}
+
+int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, double* last_dev) {
+  if (!family_link_valid(o.family, o.link)) {
+    set_error("requirement failed: unsupported family/link combination");
+    return SGLM_EINVAL;
+  }
+  const int64_t p = be.ncols();
+  std::vector<double> packed((size_t)packed_len(p)), gram((size_t)(p * p)), xtwz((size_t)p);
+  Solver solver(p);
+  for (int it = 0; it < iters; ++it) {
+    int rc = be.pass(MODE_IRLS, beta, 0.0, 0.0, o.family, o.link, packed.data());
+    if (rc) return rc;
+    if (last_dev) *last_dev = family_dev_factor(o.family) * packed[tri_count(p) + p + S_DEV];
+    unpack_gram(packed.data(), p, gram.data(), xtwz.data());
+    const double t0 = now_ms();
+    const int srv = solver.solve(gram.data(), xtwz.data(), beta);
+    be.solve_ms += now_ms() - t0;
+    if (srv) {
+      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return SGLM_ESINGULAR;
+    }
+  }
+  return SGLM_OK;
+}
+
+// LM.fit (LM.scala:241-274) over fitMultiple's components (LM.scala:217-237).
+int lm_drive(Backend& be, sglm_prelm* out) {
+  const int64_t p = be.ncols();
+  std::vector<double> packed((size_t)packed_len(p)), gram((size_t)(p * p)), xty((size_t)p), s(NS);
+  int rc = be.pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, packed.data());
+  if (rc) return rc;
+  unpack_gram(packed.data(), p, gram.data(), xty.data());
+  const double ysum = packed[tri_count(p) + p + S_DEV], nrow = packed[tri_count(p) + p + S_SUMW];
+  Solver solver(p);
+  std::vector<double> coefs((size_t)p), xtxi((size_t)(p * p));
+  const double t0 = now_ms();
+  // coefs = inv(X'X) * X'y (LM.scala:225-227); the Cholesky solve is the same product.
+  const int srv = solver.solve(gram.data(), xty.data(), coefs.data());
+  if (srv) {
+    set_error("breeze.linalg.MatrixSingularException: X'X is singular");
+    return SGLM_ESINGULAR;
+  }
+  solver.inverse(xtxi.data());
+  be.solve_ms += now_ms() - t0;
+  const double ymean = ysum / nrow;  // LM.scala:167-168
+  rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
+  if (rc) return rc;
+  const double sse = s[S_DEV], top = s[S_PEARSON], bot = s[S_LL];
+  const double r2 = top / bot;                                                      // LM.scala:185
+  const double fstat = ((bot - sse) / ((double)p - 1.0)) / (sse / (nrow - (double)p));  // LM.scala:186
+  const double sig2 = sse / (nrow - (double)p);                                      // LM.scala:260
+  for (int64_t i = 0; i < p; ++i) {
+    out->coefs[i] = coefs[i];
+    out->std_err[i] = std::sqrt(sig2 * xtxi[i + i * p]);  // LM.scala:262-263
+  }
+  if (out->xtxi) std::memcpy(out->xtxi, xtxi.data(), sizeof(double) * (size_t)(p * p));
+  out->sse = sse;
+  out->r2 = r2;
+  out->fstat = fstat;
+  out->sigma = std::sqrt(sig2);
+  out->nrow = nrow;
+  out->npart = be.npart();
+  return SGLM_OK;
+}
+
+}  // namespace sglm

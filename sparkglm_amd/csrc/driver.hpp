@@ -1,0 +1,41 @@
+// driver.hpp -- backend-agnostic IRLS / least-squares drivers (host side).
+#pragma once
+#include <cstdint>
+#include <string>
+
+#include "../../include/sglm.h"
+#include "common.hpp"
+
+namespace sglm {
+
+void set_error(const std::string& msg);
+const char* get_error();
+
+// A producer of all-reduced pass results.  The HIP engine implements it over its
+// resident shard + communicator; sglm_fit_*_external adapts caller callbacks.
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual int64_t ncols() const = 0;
+  virtual int npart() const = 0;  // number of shards (ranks) joined by the communicator
+  // {sum y, rows} over all shards
+  virtual int global_sums(double* out2) = 0;
+  // One pass in the packed wire format (lower tri X'WX | X'Wz | NS scalars), all-reduced.
+  virtual int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) = 0;
+  // Final statistics (pearson, loglik ingredients, ...) at the state of the last pass
+  // (MODE_IRLS / init modes) or at beta (MODE_LM_RESID), all-reduced, NS scalars.
+  virtual int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) = 0;
+  // host-side timers (ms) for sglm_stats
+  double solve_ms = 0.0;
+};
+
+int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out);
+int lm_drive(Backend& be, sglm_prelm* out);
+// Bench / test helper: `iters` IRLS iterations (pass at beta, then solve) from beta.
+int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, double* last_dev);
+
+void unpack_gram(const double* packed, int64_t p, double* gram, double* xtwz);
+int family_link_valid(int family, int link);
+double family_dev_factor(int family);
+
+}  // namespace sglm

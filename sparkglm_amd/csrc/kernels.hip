@@ -1,0 +1,514 @@
+// kernels.hip -- gfx950 (MI355X) kernels of the sparkGLM fitting engine.
+//
+// K1+K2 fused IRLS pass (irls_pass_kernel<P16>): one streaming pass over the HBM-resident
+// design X per IRLS iteration.  Per row block of RB=32 rows:
+//   1. LDS-DMA (global_load_lds_dwordx4) of the block's 32 x (16*P16) tile and its y/m/
+//      offset/prior values, double-buffered one block ahead;
+//   2. eta = X beta + offset (etaCreate, GLM.scala:321-332), inverse link, variance,
+//      working weight w and response z (zwCreateBinomial, GLM.scala:359-395) and the
+//      deviance / Pearson / loglik partial sums (GLM.scala:90-170) -- rowmath.hpp;
+//   3. the weighted Gramian X'WX (lower-triangular 16x16 tiles) on fp64 MFMA
+//      (v_mfma_f64_16x16x4_f64) with the accumulators resident in registers for the
+//      whole launch, and X'Wz on the VALU (partitionComponents, utils.scala:84-92).
+// Each workgroup streams a contiguous range of row blocks (split-K over rows) and writes
+// one partial; reduce_partials_kernel sums the partials in a fixed order (deterministic)
+// into the packed wire format (lower-triangular X'WX row-major | X'Wz | scalars).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "rowmath.hpp"
+
+namespace sglm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+// ---------------------------------------------------------------------------------
+// compile-time geometry.  P16 (even) column blocks of 16; NW = P16/2 waves.  Wave w
+// owns the block rows lo = w and hi = P16-1-w of the lower-triangular tile grid:
+// tiles (lo, 0..lo) and (hi, 0..hi), i.e. P16+1 tiles per wave, for the whole launch.
+// ---------------------------------------------------------------------------------
+template <int P16>
+struct Geo {
+  static_assert(P16 >= 2 && P16 % 2 == 0, "even column-block count");
+  static constexpr int NW = P16 / 2;               // waves per workgroup
+  static constexpr int NC = P16 * 16;              // padded columns
+  static constexpr int NCE = (NC + 31) / 32 * 32;  // columns in the LDS image (eta stripes)
+  static constexpr int T = P16 * (P16 + 1) / 2;    // lower-triangular 16x16 tiles
+  static constexpr int TPW = P16 + 1;              // tiles per wave
+  static constexpr int QPW = 8;                    // X column quads DMA'd per wave per block (4*P16/NW)
+  static constexpr int VPW = NW >= 4 ? 1 : 4 / NW; // vectors (y, m, offset, prior) DMA'd per wave (w < 4)
+  static constexpr int NWP2 = NW >= 8 ? 8 : (NW >= 4 ? 4 : (NW >= 2 ? 2 : 1));  // pow2 <= NW
+  static constexpr int RW = RB / NWP2;             // rows per wave in the elementwise phase (waves >= NWP2 idle)
+  static constexpr int CPG = RW / 2;               // columns per lane group per 32-column stripe
+  static constexpr int XB = NCE * RB;              // doubles per X buffer
+  // LDS layout, in doubles (one __shared__ array: keeps hipcc's LDS-DMA waits counted)
+  static constexpr int OFF_X = 0;                  // [2][XB]
+  static constexpr int OFF_V = 2 * XB;             // [2][4][RB]  y, m, offset, prior
+  static constexpr int OFF_BETA = OFF_V + 8 * RB;  // [NCE]
+  static constexpr int OFF_W = OFF_BETA + NCE;     // [RB]
+  static constexpr int OFF_WZ = OFF_W + RB;        // [RB]
+  static constexpr int OFF_RED = OFF_WZ + RB;      // [NW][NS]
+  static constexpr int LDS_DOUBLES = OFF_RED + NW * NS;
+  static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
+  // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
+  static constexpr int WG_PER_CU = (8 / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? 8 / NW : 160 * 1024 / (LDS_DOUBLES * 8);
+  static constexpr int WAVES_PER_SIMD = (WG_PER_CU * NW + 3) / 4;
+};
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left open (gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Workgroup barrier that orders LDS traffic but leaves LDS-DMA loads in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------
+// LDS-DMA staging of one row block.  X tile image: column c occupies 32 doubles at
+// c*32; row r of column c sits in slot r ^ (2c & 31) (XOR swizzle applied on the
+// source address, rule 21), which makes both the MFMA fragment reads (16 columns x 2
+// rows per half-wave) and the eta reads (RW rows x 64/RW column groups) conflict free.
+// ---------------------------------------------------------------------------------
+template <int P16>
+__device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs& a, int64_t blk, int wv,
+                                            int lane) {
+  using G = Geo<P16>;
+  const int64_t r0 = blk * RB;
+  double* xdst = lds + G::OFF_X + buf * G::XB;
+  const int i = lane & 15;
+#pragma unroll
+  for (int k = 0; k < G::QPW; ++k) {
+    const int q = wv * G::QPW + k;         // column quad
+    const int c = 4 * q + (lane >> 4);
+    const int cs = c < a.p ? c : a.p - 1;  // padded columns duplicate a valid one (never output)
+    const int srow = (2 * i) ^ ((2 * c) & 31);
+    const double* src = a.X + (int64_t)cs * a.ld + r0 + srow;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + q * 128), 16, 0, 0);
+  }
+  if (wv < 4) {
+#pragma unroll
+    for (int k = 0; k < G::VPW; ++k) {
+      // vector v: 0 y, 1 m, 2 offset, 3 prior (absent vectors re-load y)
+      const int v = wv * G::VPW + k;
+      const double* src = a.y;
+      if (v == 1 && a.m) src = a.m;
+      if (v == 2 && a.off) src = a.off;
+      if (v == 3 && a.prior) src = a.prior;
+      if (lane < 16) {
+        __builtin_amdgcn_global_load_lds((const void*)(src + r0 + 2 * lane),
+                                         (lds_void*)(lds + G::OFF_V + buf * 4 * RB + v * RB), 16, 0, 0);
+      }
+    }
+  }
+}
+
+template <int P16>
+__device__ __forceinline__ void wait_block(int wv, bool last) {
+  using G = Geo<P16>;
+  if (last) {
+    wait_vmcnt<0>();
+  } else if (wv < 4) {
+    wait_vmcnt<G::QPW + G::VPW>();
+  } else {
+    wait_vmcnt<G::QPW>();
+  }
+}
+
+// Elementwise phase: wave wv owns rows RW*wv .. RW*wv+RW-1 of the block; 64/RW lanes
+// per row form the dot product over the column groups {32t + CPG*g + u}.
+template <int P16, int FAM, int LNK>
+__device__ __forceinline__ void eta_phase(double* lds, int buf, const PassArgs& a, int64_t blk, int wv,
+                                          int lane, double& s_dev, double& s_aux) {
+  using G = Geo<P16>;
+  const double* xs = lds + G::OFF_X + buf * G::XB;
+  const double* beta = lds + G::OFF_BETA;
+  if (wv >= G::NWP2) return;
+  const int rl = lane % G::RW, g = lane / G::RW;
+  const int r = G::RW * wv + rl;
+  double eta = 0.0;
+  if (a.mode == MODE_IRLS || a.mode == MODE_LM_RESID) {
+#pragma unroll
+    for (int u = 0; u < G::CPG; ++u) {
+      const int c0 = G::CPG * g + u;  // column in stripe 0; stripe t adds 32 columns, same slot
+      const double* base = xs + c0 * 32 + (r ^ ((2 * c0) & 31));
+#pragma unroll
+      for (int t = 0; t < G::NCE / 32; ++t) eta += base[1024 * t] * beta[c0 + 32 * t];  // beta is 0 past p
+    }
+#pragma unroll
+    for (int o = G::RW; o < 64; o <<= 1) eta += __shfl_xor(eta, o);
+  }
+  if (lane < G::RW) {
+    const double* vv = lds + G::OFF_V + buf * 4 * RB;
+    const int64_t row = blk * RB + r;
+    double w = 0.0, wz = 0.0;
+    if (row < a.n) {
+      const double y = vv[r];
+      const double m = a.m ? vv[RB + r] : 1.0;
+      const double off = a.off ? vv[2 * RB + r] : 0.0;
+      const double pw = a.prior ? vv[3 * RB + r] : 1.0;
+      if (a.mode == MODE_IRLS) {
+        eta = eta + off;
+        if (a.eta_out) a.eta_out[row] = eta;
+      }
+      pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, w, wz, s_dev, s_aux);
+    }
+    lds[G::OFF_W + r] = w;
+    lds[G::OFF_WZ + r] = wz;
+  }
+}
+
+// MFMA phase.  Lane l reads X[k0 + (l>>4)][16b + (l&15)] for the blocks it needs: the
+// A operand of tile (bi,bj) is block bi as is, the B operand block bj scaled by the
+// lane's row weight.  B fragments are re-read from LDS per tile so that the block index
+// may depend on the (runtime) wave id without indexing registers.
+template <int P16>
+__device__ __forceinline__ void gram_phase(const double* lds, int buf, int wv, int lane, d4 (&acc)[Geo<P16>::TPW],
+                                           double& xz_lo, double& xz_hi) {
+  using G = Geo<P16>;
+  const double* xs = lds + G::OFF_X + buf * G::XB;
+  const double* w = lds + G::OFF_W;
+  const double* wz = lds + G::OFF_WZ;
+  const int cl = lane & 15, rq = lane >> 4;
+  const int lo = wv, hi = P16 - 1 - wv;
+  const double* colbase = xs + cl * 32;  // column c = 16b + cl has (2c & 31) == 2cl for every b
+#pragma unroll 1
+  for (int s = 0; s < RB / 4; ++s) {
+    const int r = 4 * s + rq;
+    const double* base = colbase + (r ^ (2 * cl));
+    const double wr = w[r], wzr = wz[r];
+    const double a_lo = base[512 * lo], a_hi = base[512 * hi];
+    double bf[G::TPW];
+#pragma unroll
+    for (int k = 0; k < G::TPW; ++k) bf[k] = base[512 * (k <= lo ? k : k - lo - 1)];
+    xz_lo += a_lo * wzr;
+    xz_hi += a_hi * wzr;
+#pragma unroll
+    for (int k = 0; k < G::TPW; ++k)
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= lo ? a_lo : a_hi, bf[k] * wr, acc[k], 0, 0, 0);
+  }
+}
+
+template <int P16, int FAM, int LNK>
+__global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD)) irls_pass_kernel(PassArgs a) {
+  using G = Geo<P16>;
+  __shared__ double lds[G::LDS_DOUBLES];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
+  if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
+    for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
+      lds[G::OFF_X + G::NC * RB + e] = 0.0;
+      lds[G::OFF_X + G::XB + G::NC * RB + e] = 0.0;
+    }
+  }
+  __syncthreads();
+
+  const int wg = blockIdx.x, nwg = gridDim.x;
+  const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
+  const bool do_gram = (a.mode != MODE_LM_RESID);
+
+  d4 acc[G::TPW];
+#pragma unroll
+  for (int k = 0; k < G::TPW; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
+
+  if (b0 < b1) stage_block<P16>(lds, 0, a, b0, wv, lane);
+  for (int64_t blk = b0; blk < b1; ++blk) {
+    const int buf = (int)((blk - b0) & 1);
+    const bool last = (blk + 1 >= b1);
+    if (!last) stage_block<P16>(lds, buf ^ 1, a, blk + 1, wv, lane);
+    wait_block<P16>(wv, last);
+    lds_barrier();
+    eta_phase<P16, FAM, LNK>(lds, buf, a, blk, wv, lane, s_dev, s_aux);
+    lds_barrier();
+    if (do_gram) gram_phase<P16>(lds, buf, wv, lane, acc, xz_lo, xz_hi);
+    lds_barrier();
+  }
+
+  // ---- epilogue: this workgroup's partial ----
+  double* out = a.partials + (int64_t)wg * a.stride;
+  const int lo = wv, hi = P16 - 1 - wv;
+#pragma unroll
+  for (int k = 0; k < G::TPW; ++k) {
+    const int bi = k <= lo ? lo : hi, bj = k <= lo ? k : k - lo - 1;
+    const int t = bi * (bi + 1) / 2 + bj;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j];
+  }
+  xz_lo += __shfl_xor(xz_lo, 16);
+  xz_lo += __shfl_xor(xz_lo, 32);
+  xz_hi += __shfl_xor(xz_hi, 16);
+  xz_hi += __shfl_xor(xz_hi, 32);
+  if (lane < 16) {
+    out[G::T * 256 + 16 * lo + lane] = xz_lo;
+    out[G::T * 256 + 16 * hi + lane] = xz_hi;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    s_dev += __shfl_xor(s_dev, o);
+    s_aux += __shfl_xor(s_aux, o);
+  }
+  if (lane == 0) {
+    lds[G::OFF_RED + wv * NS + 0] = s_dev;
+    lds[G::OFF_RED + wv * NS + 1] = s_aux;
+  }
+  lds_barrier();
+  if (wv == 0 && lane < NS) {
+    // slot mapping: S_DEV <- s_dev; S_SUMW (IRLS) or S_PEARSON/S_LL (LM modes) <- s_aux
+    double sd = 0.0, sa = 0.0;
+    for (int k = 0; k < G::NW; ++k) {
+      sd += lds[G::OFF_RED + k * NS + 0];
+      sa += lds[G::OFF_RED + k * NS + 1];
+    }
+    double v = 0.0;
+    if (lane == S_DEV) v = sd;
+    if (lane == S_SUMW) v = sa;
+    out[G::T * 256 + G::NC + lane] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Fixed-order reduction of the workgroup partials into the packed wire format.
+// ---------------------------------------------------------------------------------
+__global__ void reduce_partials_kernel(const double* __restrict__ part, int64_t stride, int nparts, int p,
+                                       int P16, double* __restrict__ out) {
+  // partial layout: T tiles of 256 | X'Wz [16*P16] | NS scalars
+  const int64_t tri = (int64_t)p * (p + 1) / 2;
+  const int64_t total = tri + p + NS;
+  const int T = P16 * (P16 + 1) / 2;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t src;
+    if (e < tri) {
+      int64_t i = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+      while (i * (i + 1) / 2 > e) --i;
+      while ((i + 1) * (i + 2) / 2 <= e) ++i;
+      const int64_t j = e - i * (i + 1) / 2;
+      const int64_t bi = i >> 4, bj = j >> 4;
+      const int64_t t = bi * (bi + 1) / 2 + bj;
+      src = t * 256 + (i & 15) * 16 + (j & 15);
+    } else if (e < tri + p) {
+      src = (int64_t)T * 256 + (e - tri);
+    } else {
+      src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
+    }
+    double s = 0.0;
+    for (int g = 0; g < nparts; ++g) s += part[(int64_t)g * stride + src];
+    out[e] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// eta = X beta (+ offset): LM.predict (LM.scala:39-61) / etaCreate.
+// ---------------------------------------------------------------------------------
+__global__ void predict_kernel(const double* __restrict__ X, int64_t ld, int p, int64_t n,
+                               const double* __restrict__ beta, const double* __restrict__ off,
+                               double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int j = 0; j < p; ++j) s += X[(int64_t)j * ld + i] * beta[j];
+    out[i] = off ? s + off[i] : s;
+  }
+}
+
+// Block partial sums of y (GLM.scala:420-423 ySums) -- fixed order per block.
+__global__ void ysum_kernel(const double* __restrict__ y, int64_t n, double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t a = per * blockIdx.x, b = (a + per < n) ? a + per : n;
+  for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) s += y[i];
+  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Final-statistics pass over the resident vectors and the last pass's eta: one partial
+// of NS scalars per block, summed in a fixed order on the host side reduction.
+__global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
+  __shared__ double red[4][NS];
+  RowAcc acc;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc.s[k] = 0.0;
+  const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = (lo + per < a.n) ? lo + per : a.n;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const double m = a.m ? a.m[i] : 1.0;
+    const double pw = a.prior ? a.prior[i] : 1.0;
+    const double eta = a.eta ? a.eta[i] : 0.0;
+    stats_row(a.family, a.link, a.mode, eta, a.y[i], m, pw, a.mu0, a.ybar, a.m != nullptr, acc);
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    double v = acc.s[k];
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    const int k = threadIdx.x;
+    a.partials[(int64_t)blockIdx.x * NS + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Seeded synthetic design (bit-identical to sparkglm_amd/synth.py; no FMA contraction).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ double unif(uint64_t key) { return (double)(splitmix64(key) >> 11) * 0x1.0p-53; }
+
+__global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X,
+                             int64_t ld, double* y, double* m, double* off, double* prior) {
+#pragma clang fp contract(off)
+  const uint64_t kx = splitmix64(seed), ky = splitmix64(seed ^ 0x5555555555555555ull),
+                 ko = splitmix64(seed ^ 0x3333333333333333ull), kp = splitmix64(seed ^ 0x0F0F0F0F0F0F0F0Full);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t gi = (uint64_t)(row0 + i);
+    double eta = 0.0;
+    for (int j = 0; j < p; ++j) {
+      double x;
+      if (j == 0) {
+        x = 1.0;
+      } else {
+        x = (2.0 * unif(kx + gi * (uint64_t)p + (uint64_t)j) - 1.0) * scale;
+      }
+      X[(int64_t)j * ld + i] = x;
+      const double bj = (j == 0) ? -0.25 : 0.5 * (double)((j % 5) - 2);
+      const double prod = x * bj;
+      eta = eta + prod;
+    }
+    const double u = unif(ky + gi);
+    if (kind == 0) {
+      double pr = 0.5 + 0.25 * eta;
+      pr = pr < 0.02 ? 0.02 : (pr > 0.98 ? 0.98 : pr);
+      y[i] = u < pr ? 1.0 : 0.0;
+    } else if (kind == 1) {
+      y[i] = eta + (2.0 * u - 1.0);
+    } else {
+      double lam = 1.0 + 0.5 * eta;
+      lam = lam < 0.1 ? 0.1 : lam;
+      y[i] = floor(u * 2.0 * lam);
+      if (off) off[i] = (2.0 * unif(ko + gi) - 1.0) * 0.1;
+      if (prior) prior[i] = 0.5 + unif(kp + gi);
+    }
+    if (m) m[i] = 1.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------
+// Kernel variants: P16 even in 2..16 (p <= 256); NW = P16/2 waves per workgroup.
+int pass_variant(int p) {
+  int P16 = (p + 15) / 16;
+  if (P16 & 1) ++P16;
+  return P16 < 2 ? 2 : P16;
+}
+int pass_waves(int P16) { return P16 / 2; }
+int pass_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS; }
+
+template <int P16>
+static int wg_per_cu_t() { return Geo<P16>::WG_PER_CU; }
+
+int pass_wg_per_cu(int P16) {
+  switch (P16) {
+    case 2: return wg_per_cu_t<2>();
+    case 4: return wg_per_cu_t<4>();
+    case 6: return wg_per_cu_t<6>();
+    case 8: return wg_per_cu_t<8>();
+    case 10: return wg_per_cu_t<10>();
+    case 12: return wg_per_cu_t<12>();
+    case 14: return wg_per_cu_t<14>();
+    default: return wg_per_cu_t<16>();
+  }
+}
+
+// One kernel per (column-block count, family/link): the row stage is compiled for a
+// single family so its registers fit beside the resident Gram accumulators.
+template <int P16>
+static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st) {
+  const dim3 g(grid), b(64 * Geo<P16>::NW);
+  const int mode_fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
+  const int mode_lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
+  else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, a);
+  else if (mode_fam == FAM_BINOMIAL)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, a);
+  else if (mode_fam == FAM_GAUSSIAN)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, a);
+  else if (mode_fam == FAM_POISSON)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, a);
+  else if (mode_fam == FAM_GAMMA)
+    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st) {
+  switch (P16) {
+    case 2: return launch_pass_p<2>(a, grid, st);
+    case 4: return launch_pass_p<4>(a, grid, st);
+    case 6: return launch_pass_p<6>(a, grid, st);
+    case 8: return launch_pass_p<8>(a, grid, st);
+    case 10: return launch_pass_p<10>(a, grid, st);
+    case 12: return launch_pass_p<12>(a, grid, st);
+    case 14: return launch_pass_p<14>(a, grid, st);
+    case 16: return launch_pass_p<16>(a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st) {
+  const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks), dim3(256), 0, st, part, stride, nparts, p, P16, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
+                          double* out, hipStream_t st) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, ld, p, n, beta, off, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hipStream_t st) {
+  hipLaunchKernelGGL(ysum_kernel, dim3(nparts), dim3(256), 0, st, y, n, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,
+                        double* y, double* m, double* off, double* prior, hipStream_t st) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, kind, row0, n, p, seed, scale, X, ld, y,
+                     m, off, prior);
+  return hipGetLastError();
+}
+
+}  // namespace sglm

@@ -1,0 +1,24 @@
+// kernels.hpp -- host-side launchers of the gfx950 kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace sglm {
+
+int pass_variant(int p);        // column-block count P16 of the kernel instantiated for p
+int pass_waves(int P16);        // waves per workgroup of that variant
+int pass_stride(int P16);       // doubles per workgroup partial
+int pass_wg_per_cu(int P16);    // workgroups per CU the variant is built for
+hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st);
+hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
+hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st);
+hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
+                          double* out, hipStream_t st);
+hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hipStream_t st);
+hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,
+                        double* y, double* m, double* off, double* prior, hipStream_t st);
+
+}  // namespace sglm

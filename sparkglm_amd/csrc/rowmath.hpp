@@ -1,0 +1,174 @@
+// rowmath.hpp -- per-row family/link arithmetic of the IRLS pass (device side).
+//
+// Mirrors the reference's elementwise stage operation-for-operation:
+//   link / lPrime / unlink  GLM.scala:190-251   (logit, probit, cloglog)
+//   varianceBinomial        GLM.scala:125-129
+//   w = 1/(V g'^2), z = eta + (y - mu) g' - offset      GLM.scala:289-290, 370-371
+//   devBinomial row value   GLM.scala:166-167   (summed, times 2 on the host)
+//   pearsonCalc             GLM.scala:90-101
+//   llBinomial              GLM.scala:132-143   (Breeze Binomial(m.toInt, mu).logProbabilityOf)
+// Extension families (gaussian/identity, poisson/log, gamma/inverse, prior weights)
+// follow R's family objects on the same skeleton.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace sglm {
+
+// Breeze Gaussian(0,1) as used by the probit link.
+__device__ __forceinline__ double norm_cdf(double x) { return 0.5 * (1.0 + erf(x / sqrt(2.0))); }
+__device__ __forceinline__ double norm_icdf(double q) { return 0.0 + 1.0 * sqrt(2.0) * erfinv(2.0 * q - 1.0); }
+__device__ __forceinline__ double norm_pdf(double x) {
+  double d = (x - 0.0) / 1.0;
+  return exp(-d * d / 2.0 - (log(sqrt(2.0 * M_PI)) + log(1.0)));
+}
+
+__device__ __forceinline__ double link_fn(int fam, int lnk, double mu, double m) {
+  if (fam == FAM_BINOMIAL) {
+    if (lnk == LNK_LOGIT) return log(mu / (m + (-1.0 * mu)));
+    if (lnk == LNK_PROBIT) return norm_icdf(mu / m);
+    return log(-1.0 * log(1.0 + (-1.0 * (mu / m))));
+  }
+  if (fam == FAM_GAUSSIAN) return mu;
+  if (fam == FAM_POISSON) return log(mu);
+  return 1.0 / mu;
+}
+
+__device__ __forceinline__ double unlink_fn(int fam, int lnk, double eta, double m) {
+  if (fam == FAM_BINOMIAL) {
+    if (lnk == LNK_LOGIT) return m / (1.0 + exp(-1.0 * eta));
+    if (lnk == LNK_PROBIT) return m * norm_cdf(eta);
+    return m * (1.0 + (-1.0 * exp(-exp(eta))));
+  }
+  if (fam == FAM_GAUSSIAN) return eta;
+  if (fam == FAM_POISSON) return exp(eta);
+  return 1.0 / eta;
+}
+
+__device__ __forceinline__ double lprime_fn(int fam, int lnk, double mu, double m) {
+  if (fam == FAM_BINOMIAL) {
+    if (lnk == LNK_LOGIT) return m / (mu * (m + (-1.0 * mu)));
+    if (lnk == LNK_PROBIT) return 1.0 / (m * norm_pdf(norm_icdf(mu / m)));
+    return 1.0 / ((mu + (-1.0 * m)) * log(1.0 + (-1.0 * (mu / m))));
+  }
+  if (fam == FAM_GAUSSIAN) return 1.0;
+  if (fam == FAM_POISSON) return 1.0 / mu;
+  return -1.0 / (mu * mu);
+}
+
+__device__ __forceinline__ double variance_fn(int fam, double mu, double m) {
+  if (fam == FAM_BINOMIAL) return mu * (1.0 + (-1.0 * (mu / m)));
+  if (fam == FAM_GAUSSIAN) return 1.0;
+  if (fam == FAM_POISSON) return mu;
+  return mu * mu;
+}
+
+// Breeze Binomial(n, p).logProbabilityOf(k) with n = m.toInt, k = y.toInt, p = mu.
+__device__ __forceinline__ double binom_logpmf(double mval, double mu, double yval, double& bad) {
+  int n = (int)mval, k = (int)yval;
+  if (n <= 0 || k < 0 || k > n || mu < 0.0) { bad += 1.0; return 0.0; }
+  if (mu == 0.0) return k == 0 ? 0.0 : -INFINITY;
+  if (mu == 1.0) return k == n ? 0.0 : -INFINITY;
+  return lgamma(n + 1.0) - lgamma(k + 1.0) - lgamma(n - k + 1.0) + k * log(mu) + (n - k) * log1p(-mu);
+}
+
+struct RowAcc {
+  double s[NS];
+};
+
+// Unit deviance row value: devBinomial (GLM.scala:166-167) and the R families; the
+// family factor (2 for binomial / poisson / gamma) is applied on the host after summing.
+__device__ __forceinline__ double unit_dev(int fam, double y, double mu, double m, double pw) {
+  if (fam == FAM_BINOMIAL) {
+    double my = m + (-1.0 * y);
+    return pw * ((y * log(fmax(y, 1.0) / mu)) + (my * log(fmax(my, 1.0) / (m + (-1.0 * mu)))));
+  }
+  if (fam == FAM_GAUSSIAN) {
+    double e = y - mu;
+    return pw * (e * e);
+  }
+  if (fam == FAM_POISSON) return pw * ((y > 0.0 ? y * log(y / mu) : 0.0) - (y - mu));
+  return pw * (-(log(y / mu) - (y - mu) / mu));
+}
+
+// The row stage of the fused pass (zwCreateBinomial, GLM.scala:359-395 / the single-
+// partition loop body GLM.scala:282-301): w and w*z for the Gramian, and the deviance.
+// LM gram mode: w = 1, z = y, and the sums of y and of rows (LM.scala:142-155, 167).
+__device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta, double y, double m, double off,
+                                         double pw, double mu0, double ybar, double& w, double& wz, double& s_dev,
+                                         double& s_aux) {
+  (void)ybar;
+  if (mode == MODE_LM_GRAM) {
+    w = 1.0;
+    wz = y;
+    s_dev += y;
+    s_aux += 1.0;
+    return;
+  }
+  double mu;
+  if (mode == MODE_IRLS) {
+    mu = unlink_fn(fam, lnk, eta, m);
+  } else {
+    eta = link_fn(fam, lnk, mu0, m);  // offset ignored at init (GLM.scala:264-270)
+    mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, eta, m);
+  }
+  const double g = lprime_fn(fam, lnk, mu, m);
+  const double v = variance_fn(fam, mu, m);
+  w = pw * (1.0 / (v * (g * g)));
+  const double z = (eta + ((y + (-1.0 * mu)) * g)) + (-1.0 * off);
+  wz = w * z;
+  s_dev += unit_dev(fam, y, mu, m, pw);
+  s_aux += pw;
+}
+
+// Final statistics of one row at the converged mu: pearsonCalc (GLM.scala:90-101),
+// llBinomial (GLM.scala:132-143) and the extension families' loglik ingredients; LM
+// mode: SSE / SSR / SST terms of rowPartitionedSSE (LM.scala:172-175) with eta = X*coefs.
+__device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta, double y, double m, double pw,
+                                          double mu0, double ybar, bool has_m, RowAcc& acc) {
+  if (mode == MODE_LM_RESID) {
+    const double e = y - eta, t = eta + (-1.0 * ybar), b = y + (-1.0 * ybar);
+    acc.s[S_DEV] += e * e;
+    acc.s[S_PEARSON] += t * t;
+    acc.s[S_LL] += b * b;
+    acc.s[S_SUMW] += 1.0;
+    return;
+  }
+  double mu;
+  if (mode == MODE_IRLS) {
+    mu = unlink_fn(fam, lnk, eta, m);
+  } else {
+    const double e0 = link_fn(fam, lnk, mu0, m);
+    mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, e0, m);
+  }
+  const double v = variance_fn(fam, mu, m);
+  const double r = y + (-1.0 * mu);
+  acc.s[S_DEV] += unit_dev(fam, y, mu, m, pw);
+  acc.s[S_PEARSON] += pw * (r * r) / v;
+  acc.s[S_SUMW] += pw;
+  if (fam == FAM_BINOMIAL) {
+    double bad = 0.0, ll;
+    if (has_m) {
+      ll = binom_logpmf(m, mu, y, bad);
+    } else {  // m == 1: the lgamma terms vanish; same special cases as Breeze
+      const int k = (int)y;
+      if (k < 0 || k > 1 || mu < 0.0) { bad = 1.0; ll = 0.0; }
+      else if (mu == 0.0) ll = k == 0 ? 0.0 : -INFINITY;
+      else if (mu == 1.0) ll = k == 1 ? 0.0 : -INFINITY;
+      else ll = k * log(mu) + (1 - k) * log1p(-mu);
+    }
+    acc.s[S_LL] += pw * ll;
+    acc.s[S_BAD] += bad;
+  } else if (fam == FAM_GAUSSIAN) {
+    acc.s[S_LL] += log(pw);
+  } else if (fam == FAM_POISSON) {
+    acc.s[S_LL] += pw * (y * log(mu) - mu - lgamma(y + 1.0));
+  } else {
+    acc.s[S_LL] += pw * log(y);
+    acc.s[S_AUX0] += pw * (y / mu);
+    acc.s[S_AUX1] += pw * log(mu);
+  }
+}
+
+}  // namespace sglm

@@ -1,0 +1,185 @@
+// solve.cpp -- host p x p solves for the IRLS / LM drivers.
+//
+// The reference inverts X'WX with Breeze inv() (LAPACK dgetrf + dgetri) and multiplies
+// (utils.scala:103-105, 134-136; LM.scala:197-199, 225-227).  X'WX is symmetric positive
+// definite whenever every working weight is positive, so the engine factors it with
+// Cholesky (half the flops of LU, no pivot search) and keeps the factor of the last solve
+// for the standard errors; a matrix Cholesky rejects (negative weights from the
+// reference's unguarded formulas, or numerical indefiniteness) falls back to LU with
+// partial pivoting, and an exactly singular one is reported like Breeze's
+// MatrixSingularException.
+#include "solve.hpp"
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace sglm {
+
+// Left-looking (jki) Cholesky on a column-major full matrix; lower triangle out.
+int chol_factor(double* A, int64_t p) {
+  for (int64_t j = 0; j < p; ++j) {
+    double* Aj = A + j * p;
+    for (int64_t k = 0; k < j; ++k) {
+      const double ljk = A[j + k * p];
+      if (ljk == 0.0) continue;
+      const double* Ak = A + k * p;
+      for (int64_t i = j; i < p; ++i) Aj[i] -= Ak[i] * ljk;
+    }
+    const double d = Aj[j];
+    if (!(d > 0.0) || !std::isfinite(d)) return (int)(j + 1);
+    const double s = std::sqrt(d);
+    Aj[j] = s;
+    const double inv = 1.0 / s;
+    for (int64_t i = j + 1; i < p; ++i) Aj[i] *= inv;
+  }
+  for (int64_t j = 1; j < p; ++j)
+    for (int64_t i = 0; i < j; ++i) A[i + j * p] = 0.0;
+  return 0;
+}
+
+void chol_solve(const double* L, int64_t p, const double* b, double* x) {
+  std::vector<double> t(b, b + p);
+  for (int64_t j = 0; j < p; ++j) {  // L t = b (column sweep)
+    t[j] /= L[j + j * p];
+    const double tj = t[j];
+    for (int64_t i = j + 1; i < p; ++i) t[i] -= L[i + j * p] * tj;
+  }
+  for (int64_t i = p - 1; i >= 0; --i) {  // L' x = t
+    double s = t[i];
+    const double* Li = L + i * p;
+    for (int64_t k = i + 1; k < p; ++k) s -= Li[k] * t[k];
+    t[i] = s / L[i + i * p];
+  }
+  std::memcpy(x, t.data(), sizeof(double) * p);
+}
+
+// inv(L) in place-free form: returns M = inv(L) (lower), column-major.
+static void tri_inverse(const double* L, int64_t p, std::vector<double>& M) {
+  M.assign((size_t)(p * p), 0.0);
+  for (int64_t j = 0; j < p; ++j) {
+    double* Mj = M.data() + j * p;
+    Mj[j] = 1.0 / L[j + j * p];
+    for (int64_t i = j + 1; i < p; ++i) {
+      // M[i][j] = -(sum_{k=j}^{i-1} L[i][k] M[k][j]) / L[i][i]
+      double s = 0.0;
+      for (int64_t k = j; k < i; ++k) s += L[i + k * p] * Mj[k];
+      Mj[i] = -s / L[i + i * p];
+    }
+  }
+}
+
+void chol_inv_diag(const double* L, int64_t p, double* diag) {
+  std::vector<double> M;
+  tri_inverse(L, p, M);
+  for (int64_t i = 0; i < p; ++i) {  // inv(A) = M' M  ->  diag_i = sum_k M[k][i]^2
+    const double* Mi = M.data() + i * p;
+    double s = 0.0;
+    for (int64_t k = i; k < p; ++k) s += Mi[k] * Mi[k];
+    diag[i] = s;
+  }
+}
+
+void chol_inverse(const double* L, int64_t p, double* Ainv) {
+  std::vector<double> M;
+  tri_inverse(L, p, M);
+  for (int64_t j = 0; j < p; ++j)
+    for (int64_t i = j; i < p; ++i) {
+      const double* Mi = M.data() + i * p;
+      const double* Mj = M.data() + j * p;
+      double s = 0.0;
+      for (int64_t k = i; k < p; ++k) s += Mi[k] * Mj[k];
+      Ainv[i + j * p] = s;
+      Ainv[j + i * p] = s;
+    }
+}
+
+int lu_inverse(double* A, int64_t p) {
+  std::vector<int64_t> piv((size_t)p);
+  for (int64_t k = 0; k < p; ++k) {
+    int64_t ip = k;
+    double amax = std::fabs(A[k + k * p]);
+    for (int64_t i = k + 1; i < p; ++i)
+      if (std::fabs(A[i + k * p]) > amax) { amax = std::fabs(A[i + k * p]); ip = i; }
+    piv[k] = ip;
+    if (A[ip + k * p] == 0.0) return 1;
+    if (ip != k)
+      for (int64_t j = 0; j < p; ++j) std::swap(A[k + j * p], A[ip + j * p]);
+    const double inv = 1.0 / A[k + k * p];
+    for (int64_t i = k + 1; i < p; ++i) A[i + k * p] *= inv;
+    for (int64_t j = k + 1; j < p; ++j) {
+      const double a = A[k + j * p];
+      if (a != 0.0)
+        for (int64_t i = k + 1; i < p; ++i) A[i + j * p] -= A[i + k * p] * a;
+    }
+  }
+  for (int64_t j = 0; j < p; ++j) {  // inv(U)
+    A[j + j * p] = 1.0 / A[j + j * p];
+    const double ajj = -A[j + j * p];
+    for (int64_t k = 0; k < j; ++k) {
+      const double t = A[k + j * p];
+      if (t != 0.0) {
+        for (int64_t i = 0; i < k; ++i) A[i + j * p] += t * A[i + k * p];
+        A[k + j * p] = t * A[k + k * p];
+      }
+    }
+    for (int64_t i = 0; i < j; ++i) A[i + j * p] *= ajj;
+  }
+  std::vector<double> work((size_t)p);
+  for (int64_t j = p - 1; j >= 0; --j) {  // inv(A) L = inv(U)
+    for (int64_t i = j + 1; i < p; ++i) { work[i] = A[i + j * p]; A[i + j * p] = 0.0; }
+    for (int64_t k = j + 1; k < p; ++k) {
+      const double t = work[k];
+      if (t != 0.0)
+        for (int64_t i = 0; i < p; ++i) A[i + j * p] -= A[i + k * p] * t;
+    }
+  }
+  for (int64_t j = p - 2; j >= 0; --j) {
+    const int64_t jp = piv[j];
+    if (jp != j)
+      for (int64_t i = 0; i < p; ++i) std::swap(A[i + j * p], A[i + jp * p]);
+  }
+  return 0;
+}
+
+int Solver::solve(const double* A, const double* b, double* x) {
+  const size_t pp = (size_t)(p_ * p_);
+  fac_.assign(A, A + pp);
+  if (chol_factor(fac_.data(), p_) == 0) {
+    kind_ = 1;
+    chol_solve(fac_.data(), p_, b, x);
+    return 0;
+  }
+  fac_.assign(A, A + pp);
+  if (lu_inverse(fac_.data(), p_) != 0) {
+    kind_ = 0;
+    return 1;
+  }
+  kind_ = 2;  // fac_ holds inv(A): coefs = inv(A) * b as the reference does
+  for (int64_t i = 0; i < p_; ++i) {
+    double s = 0.0;
+    for (int64_t k = 0; k < p_; ++k) s += fac_[i + k * p_] * b[k];
+    x[i] = s;
+  }
+  return 0;
+}
+
+void Solver::inv_diag(double* d) const {
+  if (kind_ == 1) {
+    chol_inv_diag(fac_.data(), p_, d);
+  } else if (kind_ == 2) {
+    for (int64_t i = 0; i < p_; ++i) d[i] = fac_[i + i * p_];
+  } else {
+    for (int64_t i = 0; i < p_; ++i) d[i] = 0.0;
+  }
+}
+
+void Solver::inverse(double* Ainv) const {
+  if (kind_ == 1) {
+    chol_inverse(fac_.data(), p_, Ainv);
+  } else if (kind_ == 2) {
+    std::memcpy(Ainv, fac_.data(), sizeof(double) * (size_t)(p_ * p_));
+  }
+}
+
+}  // namespace sglm

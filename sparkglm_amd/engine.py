@@ -1,0 +1,211 @@
+"""Python handle over the C ABI: one `Engine` per HIP device (one per rank).
+
+This is plumbing around libsglm_hip.so; every fit runs in the C++ driver and the gfx950
+kernels.  See include/sglm.h for the contract of each call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class FitGLM:
+    """PreGLM (GLM.scala:25-33) plus the deviance trace."""
+    coefs: np.ndarray
+    stderr: np.ndarray
+    deviance: float
+    null_deviance: float
+    pearson: float
+    loglik: float
+    iter: int
+    nrow: float
+    npart: int
+    dev_trace: np.ndarray = field(default=None)
+
+
+@dataclass
+class FitLM:
+    """PreLM (LM.scala:10-14) plus LM.fit's stdErr and sigma (LM.scala:260-263)."""
+    coefs: np.ndarray
+    xtxi: np.ndarray
+    stderr: np.ndarray
+    sse: float
+    r2: float
+    fstat: float
+    sigma: float
+    nrow: float
+    npart: int
+
+
+def _vec(a, n):
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+    if a.shape[0] != n:
+        raise L.IllegalArgumentException("requirement failed: The two DataFrames must have the same number of rows")
+    return a
+
+
+def glm_opts(family="binomial", link="logit", tol=1e-6, verbose=False, max_iter=0, init="single", npart=0):
+    fam = family.lower()
+    if fam not in L.FAMILIES:
+        raise L.IllegalArgumentException(f"requirement failed: unknown family {family!r}")
+    if link not in L.LINKS:
+        raise L.IllegalArgumentException(f"requirement failed: unknown link {link!r}")
+    return L.GlmOpts(L.FAMILIES[fam], L.LINKS[link], float(tol), int(bool(verbose)), int(max_iter),
+                     L.INIT_MULTIPLE if init == "multiple" else L.INIT_SINGLE, int(npart))
+
+
+class Engine:
+    """One HIP device holding one row shard of the design in HBM."""
+
+    def __init__(self, device: int = 0):
+        self._lib = L.load()
+        h = C.c_void_p()
+        L.check(self._lib.sglm_create(int(device), C.byref(h)), "sglm_create")
+        self._h = h
+        self.device = device
+        self.n = 0
+        self.p = 0
+        self._comm_keep = None
+
+    # ---- lifecycle ----
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sglm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- data ----
+    def set_data(self, X, y, m=None, offset=None, prior=None):
+        X = np.asfortranarray(X, dtype=np.float64)
+        if X.ndim != 2:
+            raise L.IllegalArgumentException("requirement failed: X must be a matrix")
+        n, p = X.shape
+        y, m, offset, prior = _vec(y, n), _vec(m, n), _vec(offset, n), _vec(prior, n)
+        L.check(self._lib.sglm_set_data(self._h, L.ptr(X), n, p, n, L.ptr(y), L.ptr(m), L.ptr(offset),
+                                        L.ptr(prior)), "sglm_set_data")
+        self.n, self.p = n, p
+        return self
+
+    def set_data_device(self, X, y, m=None, offset=None, prior=None):
+        """Torch CUDA tensors (column-major X as X.t().contiguous().t() or an (n, p) F-view)."""
+        n, p = X.shape
+        ldx = X.stride(1)
+        if X.stride(0) != 1:
+            raise L.IllegalArgumentException("requirement failed: X must be column-major on device")
+        g = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        L.check(self._lib.sglm_set_data_device(self._h, g(X), n, p, ldx, g(y), g(m), g(offset), g(prior)),
+                "sglm_set_data_device")
+        self.n, self.p = n, p
+        return self
+
+    def synth(self, kind: int, row0: int, n: int, p: int, seed: int):
+        L.check(self._lib.sglm_synth(self._h, int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1))),
+                "sglm_synth")
+        self.n, self.p = n, p
+        return self
+
+    def get_data(self):
+        X = np.empty((self.n, self.p), order="F")
+        y, m, off, pr = (np.empty(self.n) for _ in range(4))
+        L.check(self._lib.sglm_get_data(self._h, L.ptr(X), L.ptr(y), L.ptr(m), L.ptr(off), L.ptr(pr)))
+        return X, y, m, off, pr
+
+    # ---- communicators ----
+    def set_comm(self, fn, on_device: bool):
+        """fn(buf_ptr:int, count:int, stream:int, on_device:bool) -> None, sums in place."""
+        def _cb(ctx, buf, count, stream, dev):
+            try:
+                fn(C.cast(buf, C.c_void_p).value, int(count), stream, bool(dev))
+                return 0
+            except Exception:  # an exception cannot cross the C frame
+                import traceback
+                traceback.print_exc()
+                return 1
+        cb = L.ALLREDUCE_FN(_cb)
+        self._comm_keep = cb
+        L.check(self._lib.sglm_set_comm(self._h, cb, None, int(bool(on_device))), "sglm_set_comm")
+
+    def set_comm_rccl(self, nranks: int, rank: int, unique_id: bytes):
+        buf = C.create_string_buffer(bytes(unique_id), 128)
+        L.check(self._lib.sglm_set_comm_rccl(self._h, int(nranks), int(rank), buf), "sglm_set_comm_rccl")
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        lib = L.load()
+        buf = C.create_string_buffer(128)
+        L.check(lib.sglm_rccl_unique_id(buf), "sglm_rccl_unique_id")
+        return buf.raw
+
+    # ---- fits ----
+    def fit_glm(self, family="binomial", link="logit", tol=1e-6, verbose=False, max_iter=0, init="single",
+                npart=0, max_trace=512) -> FitGLM:
+        o = glm_opts(family, link, tol, verbose, max_iter, init, npart)
+        coefs, se = np.zeros(self.p), np.zeros(self.p)
+        trace = np.full(max_trace, np.nan)
+        pre = L.PreGLM(L.ptr(coefs), L.ptr(se), 0, 0, 0, 0, 0, 0, 0, L.ptr(trace), max_trace)
+        L.check(self._lib.sglm_fit_glm(self._h, C.byref(o), C.byref(pre)), "sglm_fit_glm")
+        return FitGLM(coefs, se, pre.deviance, pre.null_deviance, pre.pearson, pre.loglik, pre.iter, pre.nrow,
+                      pre.npart, trace[: pre.iter + 1].copy())
+
+    def fit_lm(self) -> FitLM:
+        p = self.p
+        coefs, se, xtxi = np.zeros(p), np.zeros(p), np.zeros((p, p), order="F")
+        pre = L.PreLM(L.ptr(coefs), xtxi.ctypes.data_as(L.dp), L.ptr(se), 0, 0, 0, 0, 0, 0)
+        L.check(self._lib.sglm_fit_lm(self._h, C.byref(pre)), "sglm_fit_lm")
+        return FitLM(coefs, xtxi, se, pre.sse, pre.r2, pre.fstat, pre.sigma, pre.nrow, pre.npart)
+
+    def irls_pass(self, beta=None, mu0=0.0, family="binomial", link="logit", init="single"):
+        o = glm_opts(family, link, init=init)
+        p = self.p
+        gram, xtwz, s = np.zeros((p, p), order="F"), np.zeros(p), np.zeros(L.NS)
+        b = None if beta is None else np.ascontiguousarray(beta, dtype=np.float64)
+        L.check(self._lib.sglm_irls_pass(self._h, C.byref(o), L.ptr(b), float(mu0), gram.ctypes.data_as(L.dp),
+                                         L.ptr(xtwz), L.ptr(s)), "sglm_irls_pass")
+        return gram, xtwz, s
+
+    def irls_iterations(self, beta, iters, family="binomial", link="logit"):
+        o = glm_opts(family, link)
+        b = np.ascontiguousarray(beta, dtype=np.float64).copy()
+        dev = C.c_double()
+        L.check(self._lib.sglm_irls_iterations(self._h, C.byref(o), L.ptr(b), int(iters), C.byref(dev)),
+                "sglm_irls_iterations")
+        return b, dev.value
+
+    def predict(self, beta, add_offset=False):
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        out = np.empty(self.n)
+        L.check(self._lib.sglm_predict(self._h, L.ptr(b), int(bool(add_offset)), L.ptr(out)), "sglm_predict")
+        return out
+
+    def stats(self) -> dict:
+        s = L.Stats()
+        L.check(self._lib.sglm_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in L.Stats._fields_}
+
+    def reset_stats(self):
+        L.check(self._lib.sglm_reset_stats(self._h))
+
+
+def device_count() -> int:
+    lib = L.load()
+    c = C.c_int()
+    rc = lib.sglm_device_count(C.byref(c))
+    return c.value if rc == 0 else 0

@@ -52,7 +52,7 @@ def lib():
         _lib.orc_fit_lm.argtypes = [dp, C.c_int64, C.c_int64, C.c_int64, dp, C.c_int, C.c_int,
                                     dp, dp, dp, dp, dp, dp, dp]
         _lib.orc_shard_partials.argtypes = [dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, dp,
-                                            C.c_int, C.c_int, dp, C.c_double, C.c_int, dp]
+                                            C.c_int, C.c_int, C.c_int, dp, C.c_double, C.c_double, dp]
         _lib.orc_lu_inverse.argtypes = [dp, C.c_int64]
         for f in ("orc_norm_cdf", "orc_norm_icdf", "orc_erfinv"):
             getattr(_lib, f).argtypes = [C.c_double]
@@ -123,17 +123,17 @@ def fit_lm(X, y, npart=1, nthreads=1):
                 sigma=sig.value)
 
 
-def shard_partials(X, y, family, link, beta=None, mu0=0.0, single_init=True, *, m=None, offset=None,
+def shard_partials(X, y, family, link, mode, beta=None, mu0=0.0, ybar=0.0, *, m=None, offset=None,
                    prior=None):
+    """One shard's packed partials (mode: 0 irls, 1 init-single, 2 init-multi, 3 lm-gram, 4 lm-resid)."""
     X = np.asfortranarray(X, dtype=np.float64)
     n, p = X.shape
     y = _col(y, n)
     m, offset, prior = _col(m, n), _col(offset, n), _col(prior, n)
     out = np.zeros(p * (p + 1) // 2 + p + NS)
     b = None if beta is None else np.ascontiguousarray(beta, dtype=np.float64)
-    rc = lib().orc_shard_partials(_ptr(X), n, p, max(n, 1) if n == 0 else n, _ptr(y), _ptr(m),
-                                  _ptr(offset), _ptr(prior), FAMILIES[family], LINKS[link], _ptr(b),
-                                  mu0, int(single_init), _ptr(out))
+    rc = lib().orc_shard_partials(_ptr(X), n, p, n, _ptr(y), _ptr(m), _ptr(offset), _ptr(prior),
+                                  FAMILIES[family], LINKS[link], int(mode), _ptr(b), mu0, ybar, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle orc_shard_partials failed rc={rc}")
     return out

@@ -536,23 +536,44 @@ done:
 /* Shard partials in the engine's packed wire format (for distributed tests)   */
 /* ------------------------------------------------------------------------- */
 int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx, const double *y, const double *m,
-                       const double *offset, const double *prior, int family, int link, const double *beta,
-                       double mu0, int single_init, double *packed) {
+                       const double *offset, const double *prior, int family, int link, int mode,
+                       const double *beta, double mu0, double ybar, double *packed) {
   if (n < 0 || p <= 0 || ldx < n) return ORC_EINVAL;
   orc_data d = {X, n, p, ldx, y, m, offset, prior, family, link};
   int64_t tri = p * (p + 1) / 2;
   memset(packed, 0, sizeof(double) * (size_t)(tri + p + ORC_NS));
   if (n == 0) return ORC_OK;
+  double *s = packed + tri + p;
   double *eta = malloc(sizeof(double) * n), *mu = malloc(sizeof(double) * n);
   double *w = malloc(sizeof(double) * n), *z = malloc(sizeof(double) * n), *tmp = malloc(sizeof(double) * n);
   double *Gm = calloc(p * p, sizeof(double)), *xtwz = calloc(p, sizeof(double));
-  if (beta) {
+  if (mode == ORC_MODE_LM_RESID) {
+    /* rowPartitionedSSE (LM.scala:160-188) at beta with the global mean ybar */
+    eta_create(&d, beta, eta, 0);
+    for (int64_t i = 0; i < n; ++i) { double e = y[i] - eta[i]; tmp[i] = e * e; }
+    s[ORC_S_DEV] = pairwise_sum(tmp, n);
+    for (int64_t i = 0; i < n; ++i) { double e = eta[i] + (-1.0 * ybar); tmp[i] = e * e; }
+    s[ORC_S_PEARSON] = pairwise_sum(tmp, n);
+    for (int64_t i = 0; i < n; ++i) { double e = y[i] + (-1.0 * ybar); tmp[i] = e * e; }
+    s[ORC_S_LL] = pairwise_sum(tmp, n);
+    s[ORC_S_SUMW] = (double)n;
+    goto out;
+  }
+  if (mode == ORC_MODE_LM_GRAM) {
+    /* rowPartitionedComponents (LM.scala:142-155): X'X, X'y; plus sum y and rows */
+    for (int64_t i = 0; i < n; ++i) { w[i] = 1.0; z[i] = y[i]; }
+    gram_rows(X, ldx, p, 0, n, w, z, Gm, xtwz);
+    s[ORC_S_DEV] = pairwise_sum(y, n);
+    s[ORC_S_SUMW] = (double)n;
+    goto pack;
+  }
+  if (mode == ORC_MODE_IRLS) {
     eta_create(&d, beta, eta, 1);
     for (int64_t i = 0; i < n; ++i) mu[i] = unlink_fn(family, link, eta[i], M_(&d, i));
   } else {
     for (int64_t i = 0; i < n; ++i) {
       eta[i] = link_fn(family, link, mu0, M_(&d, i));
-      mu[i] = single_init ? mu0 : unlink_fn(family, link, eta[i], M_(&d, i));
+      mu[i] = (mode == ORC_MODE_INIT_SINGLE) ? mu0 : unlink_fn(family, link, eta[i], M_(&d, i));
     }
   }
   for (int64_t i = 0; i < n; ++i) {
@@ -561,10 +582,6 @@ int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx, const
     z[i] = (eta[i] + ((y[i] + (-1.0 * mu[i])) * grad)) + (-1.0 * OFF_(&d, i));
   }
   gram_rows(X, ldx, p, 0, n, w, z, Gm, xtwz);
-  for (int64_t i = 0; i < p; ++i)
-    for (int64_t j = 0; j <= i; ++j) packed[i * (i + 1) / 2 + j] = Gm[i + j * p];
-  for (int64_t j = 0; j < p; ++j) packed[tri + j] = xtwz[j];
-  double *s = packed + tri + p;
   for (int64_t i = 0; i < n; ++i) tmp[i] = unit_dev(family, y[i], mu[i], M_(&d, i), PW_(&d, i));
   s[ORC_S_DEV] = pairwise_sum(tmp, n);
   for (int64_t i = 0; i < n; ++i) {
@@ -572,27 +589,34 @@ int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx, const
     tmp[i] = PW_(&d, i) * (r * r) / variance_fn(family, mu[i], M_(&d, i));
   }
   s[ORC_S_PEARSON] = pairwise_sum(tmp, n);
-  int bad = 0;
-  if (family == ORC_BINOMIAL) {
-    for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * binom_logpmf(M_(&d, i), mu[i], y[i], &bad);
-    s[ORC_S_LL] = pairwise_sum(tmp, n);
-  } else if (family == ORC_POISSON) {
-    for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * (y[i] * log(mu[i]) - mu[i] - lgamma(y[i] + 1.0));
-    s[ORC_S_LL] = pairwise_sum(tmp, n);
-  } else if (family == ORC_GAUSSIAN) {
-    for (int64_t i = 0; i < n; ++i) tmp[i] = log(PW_(&d, i));
-    s[ORC_S_LL] = pairwise_sum(tmp, n);
-  } else {
-    for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * log(y[i]);
-    s[ORC_S_LL] = pairwise_sum(tmp, n);
-    for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * (y[i] / mu[i]);
-    s[ORC_S_AUX0] = pairwise_sum(tmp, n);
-    for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * log(mu[i]);
-    s[ORC_S_AUX1] = pairwise_sum(tmp, n);
+  {
+    int bad = 0;
+    if (family == ORC_BINOMIAL) {
+      for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * binom_logpmf(M_(&d, i), mu[i], y[i], &bad);
+      s[ORC_S_LL] = pairwise_sum(tmp, n);
+    } else if (family == ORC_POISSON) {
+      for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * (y[i] * log(mu[i]) - mu[i] - lgamma(y[i] + 1.0));
+      s[ORC_S_LL] = pairwise_sum(tmp, n);
+    } else if (family == ORC_GAUSSIAN) {
+      for (int64_t i = 0; i < n; ++i) tmp[i] = log(PW_(&d, i));
+      s[ORC_S_LL] = pairwise_sum(tmp, n);
+    } else {
+      for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * log(y[i]);
+      s[ORC_S_LL] = pairwise_sum(tmp, n);
+      for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * (y[i] / mu[i]);
+      s[ORC_S_AUX0] = pairwise_sum(tmp, n);
+      for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i) * log(mu[i]);
+      s[ORC_S_AUX1] = pairwise_sum(tmp, n);
+    }
+    s[ORC_S_BAD] = (double)bad;
   }
-  s[ORC_S_BAD] = (double)bad;
   for (int64_t i = 0; i < n; ++i) tmp[i] = PW_(&d, i);
   s[ORC_S_SUMW] = pairwise_sum(tmp, n);
+pack:
+  for (int64_t i = 0; i < p; ++i)
+    for (int64_t j = 0; j <= i; ++j) packed[i * (i + 1) / 2 + j] = Gm[i + j * p];
+  for (int64_t j = 0; j < p; ++j) packed[tri + j] = xtwz[j];
+out:
   free(eta); free(mu); free(w); free(z); free(tmp); free(Gm); free(xtwz);
   return ORC_OK;
 }

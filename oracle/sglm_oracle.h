@@ -57,16 +57,20 @@ int orc_fit_lm(const double *X, int64_t n, int64_t p, int64_t ldx, const double 
                int nthreads, double *coefs, double *xtxi, double *stderr_, double *sse,
                double *r2, double *fstat, double *sigma);
 
+/* Pass modes (same values as the engine's sglm_backend.pass modes). */
+enum { ORC_MODE_IRLS = 0, ORC_MODE_INIT_SINGLE = 1, ORC_MODE_INIT_MULTI = 2, ORC_MODE_LM_GRAM = 3, ORC_MODE_LM_RESID = 4 };
+
 /* One shard's contribution to one IRLS pass, in the engine's packed wire format:
  *   packed[0 .. p(p+1)/2)     lower-triangular X'WX, row-major (i >= j): index i*(i+1)/2 + j
  *   packed[tri .. tri+p)      X'Wz
  *   packed[tri+p .. +8)       scalars (see ORC_S_* below)
- * beta == NULL selects the initial constant-eta pass at mu0 (GLM.scala:263-272).
- * single_init != 0 uses mu = mu0 directly (fitSingleBinomial) instead of unlink(link(mu0)). */
+ * Modes: IRLS at beta; INIT_SINGLE (mu = mu0, fitSingleBinomial) / INIT_MULTI (mu =
+ * unlink(link(mu0)), fitMultipleBinomial) constant-eta passes (GLM.scala:263-272);
+ * LM_GRAM (X'X, X'y, sum y, rows); LM_RESID (SSE, SSR, SST at beta around ybar). */
 enum { ORC_S_DEV = 0, ORC_S_PEARSON, ORC_S_LL, ORC_S_BAD, ORC_S_AUX0, ORC_S_AUX1, ORC_S_AUX2, ORC_S_SUMW, ORC_NS };
 int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx,
                        const double *y, const double *m, const double *offset, const double *prior,
-                       int family, int link, const double *beta, double mu0, int single_init,
+                       int family, int link, int mode, const double *beta, double mu0, double ybar,
                        double *packed);
 
 /* Breeze inv() semantics: LU with partial pivoting (dgetrf) + inverse (dgetri). In place, col-major. */

@@ -1,0 +1,54 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))  # the checker (tests only)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    z = np.load(os.path.join(GOLDEN, "glm_golden.npz"), allow_pickle=False)
+    cases = {}
+    for key in z.files:
+        name, field = key.split("/")
+        cases.setdefault(name, {})[field] = z[key]
+    return cases
+
+
+@pytest.fixture(scope="session")
+def iris():
+    import csv
+    with open(os.path.join(GOLDEN, "iris.csv")) as f:
+        rows = list(csv.DictReader(f))
+    cols = {k: np.array([float(r[k]) for r in rows]) for k in rows[0] if k != "Species"}
+    cols["Species"] = np.array([r["Species"] for r in rows], dtype=object)
+    return cols
+
+
+def iris_design(iris):
+    """Sepal_Width ~ Petal_Length + Petal_Width + Species (test_LM.R:10, 39-44): the R
+    modelMatrix drops the first level and adds no intercept."""
+    sp = iris["Species"]
+    X = np.column_stack([iris["Petal_Length"], iris["Petal_Width"], (sp == "versicolor").astype(float),
+                         (sp == "virginica").astype(float)])
+    return X, iris["Sepal_Width"], ["Petal_Length", "Petal_Width", "Species_versicolor", "Species_virginica"]
+
+
+def rel(a, b):
+    """Max relative difference; positions that are NaN in both (the reference's own NaN
+    quirks, e.g. llBinomial with m > 1) count as equal."""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    if not a.size:
+        return 0.0
+    both = np.isnan(a) & np.isnan(b)
+    d = np.where(both, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+    return float(np.max(np.where(np.isnan(d), np.inf, d)))

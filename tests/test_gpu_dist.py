@@ -1,0 +1,84 @@
+"""Multi-rank GPU paths on one MI355X: two rank processes sharing the device with the
+engine's host all-reduce over gloo, the native RCCL communicator, and torch's RCCL
+("nccl") group through the device-buffer callback."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, mode, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from sparkglm_amd import Engine, synth
+    from sparkglm_amd import distributed as D
+    n_global, p = 40_000, 48
+    lo, hi = D.shard_range(n_global, world, rank)
+    X, y, off, pr = synth.generate(2, lo, hi - lo, p, 5)
+    eng = Engine(0)
+    eng.set_data(X, y, offset=off, prior=pr)
+    if mode == "gloo":
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        eng.set_comm(D.torch_allreduce(), on_device=False)
+    elif mode == "rccl":
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        uid = [Engine.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.set_comm_rccl(world, rank, uid[0])
+    else:  # torch nccl group, device buffers
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        eng.set_comm(D.torch_allreduce(), on_device=True)
+    f = eng.fit_glm("poisson", "log", init="multiple")
+    q.put((rank, (f.coefs, f.stderr, np.array([f.deviance, f.null_deviance, f.pearson, f.loglik, f.iter, f.nrow,
+                                                f.npart]))))
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+def _run(mode, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+def _reference():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from sparkglm_amd import synth
+    X, y, off, pr = synth.generate(2, 0, 40_000, 48, 5)
+    return po.fit_glm(X, y, "poisson", "log", offset=off, prior=pr, npart=2, nthreads=2)
+
+
+@pytest.mark.parametrize("mode,world", [("gloo", 2), ("rccl", 1), ("nccl", 1)])
+def test_sharded_fit_equals_oracle(mode, world):
+    res = _run(mode, world)
+    ref = _reference()
+    for r in range(world):
+        coefs, se, s = res[r]
+        assert int(s[4]) == ref.iter and s[5] == 40_000 and int(s[6]) == world
+        assert rel(coefs, ref.coefs) < 1e-9 and rel(se, ref.stderr) < 1e-9
+        assert rel(s[:4], [ref.deviance, ref.null_deviance, ref.pearson, ref.loglik]) < 1e-9

@@ -52,3 +52,9 @@ def rel(a, b):
     both = np.isnan(a) & np.isnan(b)
     d = np.where(both, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
     return float(np.max(np.where(np.isnan(d), np.inf, d)))
+
+
+def nrel(a, b):
+    """Norm-wise relative difference max|a-b| / max|b| (for sums with cancellation)."""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))

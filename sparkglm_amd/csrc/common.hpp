@@ -30,9 +30,10 @@ inline int64_t packed_len(int64_t p) { return tri_count(p) + p + NS; }
 
 // Arguments of one fused pass launch.
 struct PassArgs {
-  const double* X;      // col-major, leading dimension ld, p columns
+  const double* X;      // col-major, leading dimension ld, 4*nq columns (zero past p)
   int64_t ld;
   int p;
+  int nq;               // column quads stored: ceil(p / 4)
   const double* y;
   const double* m;      // may be null (binomial trials = 1)
   const double* off;    // may be null
@@ -46,6 +47,7 @@ struct PassArgs {
   double* partials;     // [grid][stride]
   int64_t stride;
   double* eta_out;      // optional [n]: eta of MODE_IRLS rows (for the final statistics)
+  int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math
 };
 
 // Arguments of the final-statistics pass (stats_kernel).

@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -74,6 +75,7 @@ struct sglm_engine : public Backend {
   // stats
   int64_t passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0;
+  int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
 
   ~sglm_engine() override { release(); }
 
@@ -200,13 +202,14 @@ struct sglm_engine : public Backend {
     nblocks = (n + RB - 1) / RB;
     n_pad = std::max<int64_t>(nblocks, 1) * RB;
     const size_t vb = sizeof(double) * (size_t)n_pad;
-    hipError_t e = hipMalloc(&dX, vb * (size_t)p);
+    const size_t ncols = (size_t)((p + 3) / 4 * 4);  // whole column quads for the LDS-DMA staging
+    hipError_t e = hipMalloc(&dX, vb * ncols);
     if (e != hipSuccess) {
       set_error(hip_msg(e, "hipMalloc(X)"));
       free_data();
       return SGLM_ENOMEM;
     }
-    HIPCHK(hipMemsetAsync(dX, 0, vb * (size_t)p, st));
+    HIPCHK(hipMemsetAsync(dX, 0, vb * ncols, st));
     for (auto pr : {std::make_pair(&dy, true), std::make_pair(&dm, has_m), std::make_pair(&doff, has_off),
                     std::make_pair(&dprior, has_prior), std::make_pair(&deta, true)}) {
       if (!pr.second) continue;
@@ -251,6 +254,7 @@ struct sglm_engine : public Backend {
     a.X = dX;
     a.ld = n_pad;
     a.p = (int)p;
+    a.nq = (int)((p + 3) / 4);
     a.y = dy;
     a.m = dm;
     a.off = doff;
@@ -266,6 +270,7 @@ struct sglm_engine : public Backend {
     a.partials = dpart;
     a.stride = stride;
     a.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
+    a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (nblocks > 0) {
       HIPCHK(launch_pass(P16, a, grid, st));
@@ -440,6 +445,7 @@ int sglm_create(int device, sglm_engine** out) {
   hipDeviceProp_t prop;
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e, "hipGetDeviceProperties");
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  if (const char* ab = std::getenv("SGLM_DEBUG_ABLATE")) h->dbg = std::atoi(ab);
   *out = h;
   return SGLM_OK;
 }

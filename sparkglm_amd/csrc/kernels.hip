@@ -41,17 +41,19 @@ struct Geo {
   static constexpr int TPW = P16 + 1;              // tiles per wave
   static constexpr int QPW = 8;                    // X column quads DMA'd per wave per block (4*P16/NW)
   static constexpr int VPW = NW >= 4 ? 1 : 4 / NW; // vectors (y, m, offset, prior) DMA'd per wave (w < 4)
-  static constexpr int NWP2 = NW >= 8 ? 8 : (NW >= 4 ? 4 : (NW >= 2 ? 2 : 1));  // pow2 <= NW
-  static constexpr int RW = RB / NWP2;             // rows per wave in the elementwise phase (waves >= NWP2 idle)
+  // The row stage runs on the "row group": waves NW/2 .. NW/2+NRW-1 (wave 0 when NW == 1),
+  // one wave per SIMD, NRW a power of two, RW rows each.
+  static constexpr int NRW = NW >= 8 ? 4 : (NW >= 4 ? 2 : 1);
+  static constexpr int ROW0 = NW >= 2 ? NW / 2 : 0;   // first wave of the row group
+  static constexpr int RW = RB / NRW;              // rows per row-group wave
   static constexpr int CPG = RW / 2;               // columns per lane group per 32-column stripe
   static constexpr int XB = NCE * RB;              // doubles per X buffer
   // LDS layout, in doubles (one __shared__ array: keeps hipcc's LDS-DMA waits counted)
   static constexpr int OFF_X = 0;                  // [2][XB]
   static constexpr int OFF_V = 2 * XB;             // [2][4][RB]  y, m, offset, prior
   static constexpr int OFF_BETA = OFF_V + 8 * RB;  // [NCE]
-  static constexpr int OFF_W = OFF_BETA + NCE;     // [RB]
-  static constexpr int OFF_WZ = OFF_W + RB;        // [RB]
-  static constexpr int OFF_RED = OFF_WZ + RB;      // [NW][NS]
+  static constexpr int OFF_W = OFF_BETA + NCE;     // [2][w RB | w*z RB]
+  static constexpr int OFF_RED = OFF_W + 4 * RB;   // [NW][NS]
   static constexpr int LDS_DOUBLES = OFF_RED + NW * NS;
   static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
   // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
@@ -83,14 +85,15 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
   using G = Geo<P16>;
   const int64_t r0 = blk * RB;
   double* xdst = lds + G::OFF_X + buf * G::XB;
-  const int i = lane & 15;
+  const int i = lane & 15, cq = lane >> 4;
+  // lane part of the source address; the column-quad part is wave-uniform (SGPRs).
+  const double* lbase = a.X + (int64_t)cq * a.ld + r0;
 #pragma unroll
   for (int k = 0; k < G::QPW; ++k) {
-    const int q = wv * G::QPW + k;         // column quad
-    const int c = 4 * q + (lane >> 4);
-    const int cs = c < a.p ? c : a.p - 1;  // padded columns duplicate a valid one (never output)
-    const int srow = (2 * i) ^ ((2 * c) & 31);
-    const double* src = a.X + (int64_t)cs * a.ld + r0 + srow;
+    const int q = wv * G::QPW + k;                             // LDS column quad
+    const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
+    const int srow = (2 * i) ^ ((8 * q + 2 * cq) & 31);        // slot swizzle of column 4q + cq
+    const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + q * 128), 16, 0, 0);
   }
   if (wv < 4) {
@@ -122,28 +125,52 @@ __device__ __forceinline__ void wait_block(int wv, bool last) {
   }
 }
 
-// Elementwise phase: wave wv owns rows RW*wv .. RW*wv+RW-1 of the block; 64/RW lanes
-// per row form the dot product over the column groups {32t + CPG*g + u}.
+// Cross-lane sums without LDS: DPP row_ror:8 (lane i <-> i^8 inside a 16-lane row) and
+// the gfx950 permlane16/32 swaps, which hand each lane its xor-16 / xor-32 partner.
+__device__ __forceinline__ double add_xor8(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x128, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x128, 0xf, 0xf, false);
+  return v + __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double add_xor16(double v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double add_xor32(double v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
+// Row stage for one block: wave wv owns rows RW*wv .. RW*wv+RW-1; 64/RW lanes per row
+// form eta over the column groups {32t + CPG*g + u}; the first RW lanes run the family
+// arithmetic and store w and w*z for the block's MFMA phase into the w buffer `wb`.
 template <int P16, int FAM, int LNK>
-__device__ __forceinline__ void eta_phase(double* lds, int buf, const PassArgs& a, int64_t blk, int wv,
+__device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const PassArgs& a, int64_t blk, int wv,
                                           int lane, double& s_dev, double& s_aux) {
   using G = Geo<P16>;
+  const int rw = wv - G::ROW0;
+  if (rw < 0 || rw >= G::NRW) return;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* beta = lds + G::OFF_BETA;
-  if (wv >= G::NWP2) return;
   const int rl = lane % G::RW, g = lane / G::RW;
-  const int r = G::RW * wv + rl;
+  const int r = G::RW * rw + rl;
   double eta = 0.0;
-  if (a.mode == MODE_IRLS || a.mode == MODE_LM_RESID) {
+  if (a.mode == MODE_IRLS && !(a.dbg & 8)) {
+    // four independent partial sums per lane shorten the dependent FMA chain
+    double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int u = 0; u < G::CPG; ++u) {
       const int c0 = G::CPG * g + u;  // column in stripe 0; stripe t adds 32 columns, same slot
       const double* base = xs + c0 * 32 + (r ^ ((2 * c0) & 31));
 #pragma unroll
-      for (int t = 0; t < G::NCE / 32; ++t) eta += base[1024 * t] * beta[c0 + 32 * t];  // beta is 0 past p
+      for (int t = 0; t < G::NCE / 32; ++t) e4[(u * (G::NCE / 32) + t) & 3] += base[1024 * t] * beta[c0 + 32 * t];
     }
-#pragma unroll
-    for (int o = G::RW; o < 64; o <<= 1) eta += __shfl_xor(eta, o);
+    eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);  // beta is 0 past p
+    if constexpr (G::RW <= 8) eta = add_xor8(eta);
+    if constexpr (G::RW <= 16) eta = add_xor16(eta);
+    if constexpr (G::RW <= 32) eta = add_xor32(eta);
   }
   if (lane < G::RW) {
     const double* vv = lds + G::OFF_V + buf * 4 * RB;
@@ -158,86 +185,123 @@ __device__ __forceinline__ void eta_phase(double* lds, int buf, const PassArgs& 
         eta = eta + off;
         if (a.eta_out) a.eta_out[row] = eta;
       }
-      pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, w, wz, s_dev, s_aux);
+      if (a.dbg & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
     }
-    lds[G::OFF_W + r] = w;
-    lds[G::OFF_WZ + r] = wz;
+    lds[G::OFF_W + wb * 2 * RB + r] = w;
+    lds[G::OFF_W + wb * 2 * RB + RB + r] = wz;
   }
 }
 
-// MFMA phase.  Lane l reads X[k0 + (l>>4)][16b + (l&15)] for the blocks it needs: the
-// A operand of tile (bi,bj) is block bi as is, the B operand block bj scaled by the
-// lane's row weight.  B fragments are re-read from LDS per tile so that the block index
-// may depend on the (runtime) wave id without indexing registers.
-template <int P16>
-__device__ __forceinline__ void gram_phase(const double* lds, int buf, int wv, int lane, d4 (&acc)[Geo<P16>::TPW],
-                                           double& xz_lo, double& xz_hi) {
+// MFMA k-steps [S0, S1) of one block for wave WV (compile-time, so every operand is a
+// static LDS offset).  Wave WV owns block rows LO = WV and HI = P16-1-WV of the lower
+// tile grid: tiles (LO, 0..LO) then (HI, 0..HI).  Lane l reads X[k0 + (l>>4)][16b + (l&15)];
+// the A operand (blocks LO / HI) is scaled by the lane's row weight, the B operands are
+// used straight from LDS.  X'Wz accumulates on the VALU from the same A fragments.
+template <int P16, int WV>
+__device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0, int S1,
+                                           d4 (&acc)[P16 + 1], double& xz_lo, double& xz_hi) {
   using G = Geo<P16>;
+  constexpr int LO = WV, HI = P16 - 1 - WV;
   const double* xs = lds + G::OFF_X + buf * G::XB;
-  const double* w = lds + G::OFF_W;
-  const double* wz = lds + G::OFF_WZ;
+  const double* w = lds + G::OFF_W + wb * 2 * RB;
   const int cl = lane & 15, rq = lane >> 4;
-  const int lo = wv, hi = P16 - 1 - wv;
   const double* colbase = xs + cl * 32;  // column c = 16b + cl has (2c & 31) == 2cl for every b
 #pragma unroll 1
-  for (int s = 0; s < RB / 4; ++s) {
+  for (int s = S0; s < S1; ++s) {
     const int r = 4 * s + rq;
     const double* base = colbase + (r ^ (2 * cl));
-    const double wr = w[r], wzr = wz[r];
-    const double a_lo = base[512 * lo], a_hi = base[512 * hi];
-    double bf[G::TPW];
+    const double wr = w[r], wzr = w[RB + r];
+    const double x_lo = base[512 * LO], x_hi = base[512 * HI];
+    const double a_lo = x_lo * wr, a_hi = x_hi * wr;
+    xz_lo += x_lo * wzr;
+    xz_hi += x_hi * wzr;
 #pragma unroll
-    for (int k = 0; k < G::TPW; ++k) bf[k] = base[512 * (k <= lo ? k : k - lo - 1)];
-    xz_lo += a_lo * wzr;
-    xz_hi += a_hi * wzr;
-#pragma unroll
-    for (int k = 0; k < G::TPW; ++k)
-      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= lo ? a_lo : a_hi, bf[k] * wr, acc[k], 0, 0, 0);
+    for (int k = 0; k <= P16; ++k) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const double b = base[512 * (k <= LO ? k : k - LO - 1)];
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
+    }
   }
 }
 
-template <int P16, int FAM, int LNK>
-__global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD)) irls_pass_kernel(PassArgs a) {
-  using G = Geo<P16>;
-  __shared__ double lds[G::LDS_DOUBLES];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
-  if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
-    for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
-      lds[G::OFF_X + G::NC * RB + e] = 0.0;
-      lds[G::OFF_X + G::XB + G::NC * RB + e] = 0.0;
-    }
+template <int P16>
+__device__ __forceinline__ void gram_dispatch(int wv, const double* lds, int buf, int wb, int lane, int S0, int S1,
+                                              d4 (&acc)[P16 + 1], double& xz_lo, double& xz_hi) {
+  static_assert(P16 <= 16, "variant");
+  switch (wv) {
+    case 0: gram_steps<P16, 0>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 1: if constexpr (P16 >= 4) gram_steps<P16, 1>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 2: if constexpr (P16 >= 6) gram_steps<P16, 2>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 3: if constexpr (P16 >= 8) gram_steps<P16, 3>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 4: if constexpr (P16 >= 10) gram_steps<P16, 4>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 5: if constexpr (P16 >= 12) gram_steps<P16, 5>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    case 6: if constexpr (P16 >= 14) gram_steps<P16, 6>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
+    default: if constexpr (P16 >= 16) gram_steps<P16, 7>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
   }
-  __syncthreads();
+}
 
+// Pipeline per row block i (cur = i & 1):
+//   MFMA k-steps 0-3 of block i            | DMA of block i+1 landing
+//   wait for block i+1, barrier
+//   waves <  NW/2: MFMA k 4-7 of i, then the row stage of block i+1
+//   waves >= NW/2: row stage of block i+1, then MFMA k 4-7 of i     (the two halves of a
+//                  SIMD overlap MFMA with VALU work: waves w and w+4 share a SIMD)
+//   barrier; DMA of block i+2 into the buffer block i occupied.
+template <int P16, int FAM, int LNK, int WV>
+__device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv, int lane) {
+  using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
-  const bool do_gram = (a.mode != MODE_LM_RESID);
+  const bool do_gram = !(a.dbg & 2);
+  const bool early_rows = (G::NW >= 2) && (wv >= G::NW / 2);
 
-  d4 acc[G::TPW];
+  d4 acc[P16 + 1];
 #pragma unroll
-  for (int k = 0; k < G::TPW; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k <= P16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
 
-  if (b0 < b1) stage_block<P16>(lds, 0, a, b0, wv, lane);
-  for (int64_t blk = b0; blk < b1; ++blk) {
-    const int buf = (int)((blk - b0) & 1);
-    const bool last = (blk + 1 >= b1);
-    if (!last) stage_block<P16>(lds, buf ^ 1, a, blk + 1, wv, lane);
-    wait_block<P16>(wv, last);
+  // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
+  // stage of block blk+1; one call site each keeps the register allocation flat.
+  if (b0 < b1) {
+    stage_block<P16>(lds, 0, a, b0, wv, lane);
+    if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, wv, lane);
+  }
+#pragma unroll 1
+  for (int64_t blk = b0 - 1; blk < b1; ++blk) {
+    const int cur = (int)((blk - b0) & 1);  // buffers of block blk; block blk+1 uses cur ^ 1
+    const bool has_gram = blk >= b0 && do_gram;
+    const bool has_next = blk + 1 < b1;
+#pragma unroll 1
+    for (int ph = 0; ph < 3; ++ph) {
+      if (ph == 1) {
+        if (blk + 2 < b1 && blk + 1 == b0) {
+          wait_block<P16>(wv, false);  // prologue: block b0 landed, b0+1 may still fly
+        } else if (has_next) {
+          wait_vmcnt<0>();
+        }
+        lds_barrier();
+      }
+      const bool rows = has_next && ((ph == 1 && early_rows) || (ph == 2 && !early_rows));
+      const bool mfma = has_gram && (ph == 0 || (ph == 1 && !early_rows) || (ph == 2 && early_rows));
+      if (mfma) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, ph == 0 ? 0 : RB / 8, ph == 0 ? RB / 8 : RB / 4, acc,
+                                    xz_lo, xz_hi);
+      if (rows && !(a.dbg & 1)) {
+        __builtin_amdgcn_s_setprio(1);  // the row stage is on the critical path; the partner wave's MFMAs are not
+        row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
     lds_barrier();
-    eta_phase<P16, FAM, LNK>(lds, buf, a, blk, wv, lane, s_dev, s_aux);
-    lds_barrier();
-    if (do_gram) gram_phase<P16>(lds, buf, wv, lane, acc, xz_lo, xz_hi);
-    lds_barrier();
+    if (blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, wv, lane);
   }
 
-  // ---- epilogue: this workgroup's partial ----
+  // ---- epilogue: this workgroup's partial (tile t of wave wv: see gram_steps) ----
   double* out = a.partials + (int64_t)wg * a.stride;
-  const int lo = wv, hi = P16 - 1 - wv;
+  constexpr int lo = WV, hi = P16 - 1 - WV;
 #pragma unroll
-  for (int k = 0; k < G::TPW; ++k) {
+  for (int k = 0; k <= P16; ++k) {
     const int bi = k <= lo ? lo : hi, bj = k <= lo ? k : k - lo - 1;
     const int t = bi * (bi + 1) / 2 + bj;
 #pragma unroll
@@ -262,7 +326,6 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   }
   lds_barrier();
   if (wv == 0 && lane < NS) {
-    // slot mapping: S_DEV <- s_dev; S_SUMW (IRLS) or S_PEARSON/S_LL (LM modes) <- s_aux
     double sd = 0.0, sa = 0.0;
     for (int k = 0; k < G::NW; ++k) {
       sd += lds[G::OFF_RED + k * NS + 0];
@@ -272,6 +335,32 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
     if (lane == S_DEV) v = sd;
     if (lane == S_SUMW) v = sa;
     out[G::T * 256 + G::NC + lane] = v;
+  }
+}
+
+template <int P16, int FAM, int LNK>
+__global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD)) irls_pass_kernel(PassArgs a) {
+  using G = Geo<P16>;
+  __shared__ double lds[G::LDS_DOUBLES];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
+  if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
+    for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
+      lds[G::OFF_X + G::NC * RB + e] = 0.0;
+      lds[G::OFF_X + G::XB + G::NC * RB + e] = 0.0;
+    }
+  }
+  __syncthreads();
+  switch (wv) {
+    case 0: pass_body<P16, FAM, LNK, 0>(lds, a, wv, lane); break;
+    case 1: if constexpr (P16 >= 4) pass_body<P16, FAM, LNK, 1>(lds, a, wv, lane); break;
+    case 2: if constexpr (P16 >= 6) pass_body<P16, FAM, LNK, 2>(lds, a, wv, lane); break;
+    case 3: if constexpr (P16 >= 8) pass_body<P16, FAM, LNK, 3>(lds, a, wv, lane); break;
+    case 4: if constexpr (P16 >= 10) pass_body<P16, FAM, LNK, 4>(lds, a, wv, lane); break;
+    case 5: if constexpr (P16 >= 12) pass_body<P16, FAM, LNK, 5>(lds, a, wv, lane); break;
+    case 6: if constexpr (P16 >= 14) pass_body<P16, FAM, LNK, 6>(lds, a, wv, lane); break;
+    default: if constexpr (P16 >= 16) pass_body<P16, FAM, LNK, 7>(lds, a, wv, lane); break;
   }
 }
 

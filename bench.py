@@ -52,15 +52,16 @@ def cpu_baseline(p: int, seed: int, rows: int, threads: int) -> dict:
             "time_to_converge_s": dt, "iters": fit.iter}
 
 
-def pmc_traffic(p: int):
-    """Per-launch HBM bytes of the fused pass from a committed rocprofv3 --pmc summary."""
+def pmc_traffic(p: int, n: int):
+    """Per-launch HBM bytes of the fused pass: the per-row FETCH_SIZE + WRITE_SIZE measured by
+    rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
+    times the rows of this launch (the pass streams every row exactly once)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(str(p))
-        return None if e is None else e
-    except (OSError, ValueError):
+            e = json.load(f).get(str(p))
+        return None if e is None else e["bytes_per_row"] * n
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -140,7 +141,7 @@ def main() -> int:
         kern_ms = st["pass_kernel_ms"] / max(st["passes"], 1)
         flops = n * (p * (p + 1) + 2 * p)  # SYRK-convention X'WX + X'Wz per launch
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        traffic = pmc_traffic(p)
+        traffic = pmc_traffic(p, n)
         out = {
             "metric": METRIC,
             "value": total_rows * args.steps / dt,

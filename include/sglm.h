@@ -119,8 +119,12 @@ typedef struct {
   double solve_ms;          /* host wall time in the p x p solves */
   int64_t n_local;          /* rows resident on this device */
   int64_t p;
-  int workgroups;           /* fused-kernel grid size */
-  int kernel_variant;       /* column-block count P16 of the instantiated kernel */
+  int workgroups;           /* fused-kernel grid size (wide path: Gram work items) */
+  int kernel_variant;       /* fused path: column-block count P16; wide path: 0 */
+  int path;                 /* 0 fused single-panel pass (p <= 256), 1 wide panel-pair pass */
+  int wide_panels;          /* wide path: 128-column panels */
+  double row_kernel_ms;     /* wide path: total time of the row kernel (eta, w, w*z) */
+  double gram_kernel_ms;    /* wide path: total time of the panel-pair Gram kernel */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device

@@ -53,7 +53,9 @@ class PreLM(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("passes", C.c_int64), ("pass_kernel_ms", C.c_double), ("reduce_kernel_ms", C.c_double),
                 ("last_pass_ms", C.c_double), ("comm_ms", C.c_double), ("solve_ms", C.c_double),
-                ("n_local", C.c_int64), ("p", C.c_int64), ("workgroups", C.c_int), ("kernel_variant", C.c_int)]
+                ("n_local", C.c_int64), ("p", C.c_int64), ("workgroups", C.c_int), ("kernel_variant", C.c_int),
+                ("path", C.c_int), ("wide_panels", C.c_int), ("row_kernel_ms", C.c_double),
+                ("gram_kernel_ms", C.c_double)]
 
 
 class GlmDerived(C.Structure):

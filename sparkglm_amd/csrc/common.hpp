@@ -50,6 +50,43 @@ struct PassArgs {
   int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math
 };
 
+// ---- wide-design path (p > 16*MAX_P16): row kernel + panel-pair Gram kernel ----
+constexpr int WIDE_PANEL = 128;  // columns per Gram panel (8 tile blocks of 16)
+constexpr int MAX_P_WIDE = 8192;
+
+struct WideRowArgs {
+  const double* X;
+  int64_t ld;
+  int p;
+  const double* y;
+  const double* m;
+  const double* off;
+  const double* prior;
+  const double* beta;   // device [p] (MODE_IRLS)
+  int64_t n, n_pad;
+  int family, link, mode;
+  double mu0, ybar;
+  double* w;            // [n_pad] working weights (0 on padding rows)
+  double* wz;           // [n_pad] w * z
+  double* eta_out;      // optional [n]
+  double* row_partials; // [grid][NS]
+};
+
+struct WideGramArgs {
+  const double* X;
+  int64_t ld;
+  int nq;               // column quads stored
+  const double* w;
+  const double* wz;
+  int64_t nblocks;      // row blocks of RB rows
+  int npan, nst;        // panels, super-tiles npan(npan+1)/2
+  int nsplit;           // row splits per super-tile
+  int nitems;           // nst * nsplit
+  int per_xcd;          // items per XCD (grid = 8 * per_xcd)
+  double* partials;     // [nst][nsplit][stride]
+  int64_t stride;
+};
+
 // Arguments of the final-statistics pass (stats_kernel).
 struct StatsArgs {
   const double* y;

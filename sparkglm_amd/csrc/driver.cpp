@@ -49,6 +49,25 @@ void unpack_gram(const double* packed, int64_t p, double* gram, double* xtwz) {
   std::memcpy(xtwz, packed + tri_count(p), sizeof(double) * (size_t)p);
 }
 
+struct HostSolver::Impl {
+  Solver s;
+  explicit Impl(int64_t p) : s(p) {}
+};
+HostSolver::HostSolver(int64_t p) : p_(p), gram_((size_t)(p * p)), rhs_((size_t)p), impl_(new Impl(p)) {}
+HostSolver::~HostSolver() = default;
+int HostSolver::solve(const double* packed, double* x) {
+  unpack_gram(packed, p_, gram_.data(), rhs_.data());
+  return impl_->s.solve(gram_.data(), rhs_.data(), x) ? SGLM_ESINGULAR : SGLM_OK;
+}
+int HostSolver::inv_diag(double* d) {
+  impl_->s.inv_diag(d);
+  return SGLM_OK;
+}
+int HostSolver::inverse(double* Ainv) {
+  impl_->s.inverse(Ainv);
+  return SGLM_OK;
+}
+
 static double now_ms() {
   using namespace std::chrono;
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
@@ -75,8 +94,8 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
   }
   const int64_t p = be.ncols();
   const size_t pk = (size_t)packed_len(p);
-  std::vector<double> packed(pk), gram((size_t)(p * p)), xtwz((size_t)p), beta((size_t)p, 0.0), s(NS);
-  Solver solver(p);
+  std::vector<double> packed(pk), beta((size_t)p, 0.0), s(NS);
+  std::unique_ptr<SolverIface> solver = be.make_solver(p);
   double sums[2];
   int rc = be.global_sums(sums);
   if (rc) return rc;
@@ -99,13 +118,12 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
 
   while (std::fabs(deltad) > o.tol) {  // GLM.scala:281 / 452
     if (o.max_iter > 0 && iter >= o.max_iter) break;
-    unpack_gram(packed.data(), p, gram.data(), xtwz.data());
     const double t0 = now_ms();
-    const int srv = solver.solve(gram.data(), xtwz.data(), beta.data());
+    const int srv = solver->solve(packed.data(), beta.data());
     be.solve_ms += now_ms() - t0;
     if (srv) {
-      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
-      return SGLM_ESINGULAR;
+      if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return srv;
     }
     rc = be.pass(MODE_IRLS, beta.data(), ymean, 0.0, o.family, o.link, packed.data());
     if (rc) return rc;
@@ -129,7 +147,10 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
     return SGLM_EINVAL;
   }
   std::vector<double> d((size_t)p, 0.0);
-  solver.inv_diag(d.data());
+  if (iter > 0) {
+    rc = solver->inv_diag(d.data());
+    if (rc) return rc;
+  }
   for (int64_t i = 0; i < p; ++i) {
     out->coefs[i] = beta[i];
     out->std_err[i] = std::sqrt(d[i]);  // GLM.scala:307 / 464 (utils.scala:105)
@@ -150,19 +171,18 @@ int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, d
     return SGLM_EINVAL;
   }
   const int64_t p = be.ncols();
-  std::vector<double> packed((size_t)packed_len(p)), gram((size_t)(p * p)), xtwz((size_t)p);
-  Solver solver(p);
+  std::vector<double> packed((size_t)packed_len(p));
+  std::unique_ptr<SolverIface> solver = be.make_solver(p);
   for (int it = 0; it < iters; ++it) {
     int rc = be.pass(MODE_IRLS, beta, 0.0, 0.0, o.family, o.link, packed.data());
     if (rc) return rc;
     if (last_dev) *last_dev = family_dev_factor(o.family) * packed[tri_count(p) + p + S_DEV];
-    unpack_gram(packed.data(), p, gram.data(), xtwz.data());
     const double t0 = now_ms();
-    const int srv = solver.solve(gram.data(), xtwz.data(), beta);
+    const int srv = solver->solve(packed.data(), beta);
     be.solve_ms += now_ms() - t0;
     if (srv) {
-      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
-      return SGLM_ESINGULAR;
+      if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return srv;
     }
   }
   return SGLM_OK;
@@ -171,21 +191,21 @@ int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, d
 // LM.fit (LM.scala:241-274) over fitMultiple's components (LM.scala:217-237).
 int lm_drive(Backend& be, sglm_prelm* out) {
   const int64_t p = be.ncols();
-  std::vector<double> packed((size_t)packed_len(p)), gram((size_t)(p * p)), xty((size_t)p), s(NS);
+  std::vector<double> packed((size_t)packed_len(p)), s(NS);
   int rc = be.pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, packed.data());
   if (rc) return rc;
-  unpack_gram(packed.data(), p, gram.data(), xty.data());
   const double ysum = packed[tri_count(p) + p + S_DEV], nrow = packed[tri_count(p) + p + S_SUMW];
-  Solver solver(p);
+  std::unique_ptr<SolverIface> solver = be.make_solver(p);
   std::vector<double> coefs((size_t)p), xtxi((size_t)(p * p));
   const double t0 = now_ms();
   // coefs = inv(X'X) * X'y (LM.scala:225-227); the Cholesky solve is the same product.
-  const int srv = solver.solve(gram.data(), xty.data(), coefs.data());
+  const int srv = solver->solve(packed.data(), coefs.data());
   if (srv) {
-    set_error("breeze.linalg.MatrixSingularException: X'X is singular");
-    return SGLM_ESINGULAR;
+    if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'X is singular");
+    return srv;
   }
-  solver.inverse(xtxi.data());
+  rc = solver->inverse(xtxi.data());
+  if (rc) return rc;
   be.solve_ms += now_ms() - t0;
   const double ymean = ysum / nrow;  // LM.scala:167-168
   rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());

@@ -1,7 +1,9 @@
 // driver.hpp -- backend-agnostic IRLS / least-squares drivers (host side).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "../../include/sglm.h"
 #include "common.hpp"
@@ -10,6 +12,34 @@ namespace sglm {
 
 void set_error(const std::string& msg);
 const char* get_error();
+
+// The p x p solve of one iteration.  solve() takes the all-reduced packed pass output and
+// keeps what it needs for inv_diag() / inverse() of the same matrix (the standard errors
+// come from the last solve, utils.scala:103-105).  Returns SGLM_OK, SGLM_ESINGULAR, or
+// another status with the error message set.
+class SolverIface {
+ public:
+  virtual ~SolverIface() = default;
+  virtual int solve(const double* packed, double* x) = 0;
+  virtual int inv_diag(double* d) = 0;
+  virtual int inverse(double* Ainv) = 0;
+};
+
+// Host Cholesky with the LU fallback (solve.cpp).
+class HostSolver : public SolverIface {
+ public:
+  explicit HostSolver(int64_t p);
+  ~HostSolver() override;
+  int solve(const double* packed, double* x) override;
+  int inv_diag(double* d) override;
+  int inverse(double* Ainv) override;
+
+ private:
+  int64_t p_;
+  std::vector<double> gram_, rhs_;
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
 
 // A producer of all-reduced pass results.  The HIP engine implements it over its
 // resident shard + communicator; sglm_fit_*_external adapts caller callbacks.
@@ -25,6 +55,8 @@ class Backend {
   // Final statistics (pearson, loglik ingredients, ...) at the state of the last pass
   // (MODE_IRLS / init modes) or at beta (MODE_LM_RESID), all-reduced, NS scalars.
   virtual int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) = 0;
+  // The solver for this backend's systems (default: host).
+  virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats
   double solve_ms = 0.0;
 };

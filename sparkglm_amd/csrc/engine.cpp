@@ -7,14 +7,22 @@
 //   -> [device all-reduce: RCCL over xGMI] -> D2H packed -> [host all-reduce callback]
 // replacing one zwCreateBinomial + wlsComponents + treeReduce round of the reference
 // (GLM.scala:453-458, utils.scala:110-126).
+//
+// Wide designs (p > 256, or SGLM_FORCE_WIDE=1) run the panel-pair path of wide.hip
+// instead: wide_rows_kernel (eta, w, w*z) -> wide_gram_kernel (X'WX over 128x128 column
+// super-tiles) -> wide_reduce_kernel, and the p x p system is solved on the device
+// (rocSOLVER potrf/potrs, potri for the standard errors) from the reduced buffer.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -72,15 +80,23 @@ struct sglm_engine : public Backend {
   double *hbeta = nullptr, *hred = nullptr;
   int64_t part_cap = 0, red_cap = 0;
   Comm comm;
+  bool red_on_device = false;  // dred holds the all-reduced result of the last pass
+  // wide path (wide.hip)
+  bool wide = false, force_wide = false;
+  double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
+  int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
+  int npan = 0, nst = 0, nsplit = 0, nitems = 0, per_xcd = 0, rgrid = 0;
+  hipEvent_t evm = nullptr;
+  rocblas_handle blas = nullptr;
   // stats
   int64_t passes = 0;
-  double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0;
+  double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
 
   ~sglm_engine() override { release(); }
 
   void free_data() {
-    for (double** ptr : {&dX, &dy, &dm, &doff, &dprior, &deta}) {
+    for (double** ptr : {&dX, &dy, &dm, &doff, &dprior, &deta, &dw, &dwz}) {
       if (*ptr) (void)hipFree(*ptr);
       *ptr = nullptr;
     }
@@ -89,10 +105,15 @@ struct sglm_engine : public Backend {
   void release() {
     (void)hipSetDevice(device);
     free_data();
-    for (double** ptr : {&dbeta, &dpart, &dred, &dsmall}) {
+    for (double** ptr : {&dbeta, &dpart, &dred, &dsmall, &dgp, &drp}) {
       if (*ptr) (void)hipFree(*ptr);
       *ptr = nullptr;
     }
+    part_cap = red_cap = gp_cap = rp_cap = 0;
+    if (blas) (void)rocblas_destroy_handle(blas);
+    blas = nullptr;
+    if (evm) (void)hipEventDestroy(evm);
+    evm = nullptr;
     for (double** ptr : {&hbeta, &hred}) {
       if (*ptr) (void)hipHostFree(*ptr);
       *ptr = nullptr;
@@ -157,11 +178,49 @@ struct sglm_engine : public Backend {
     return allreduce_host(h, count);
   }
 
+  int ensure_wide_workspace() {
+    npan = wide_panels((int)p);
+    nst = npan * (npan + 1) / 2;
+    wstride = wide_stride();
+    // work items: ~8 per CU so the tail of unequal items stays short; >= 16 blocks each
+    const int64_t target = 8 * (int64_t)ncu;
+    int64_t ns = (target + nst - 1) / nst;
+    const int64_t max_split = std::max<int64_t>(1, nblocks / 16);
+    nsplit = (int)std::max<int64_t>(1, std::min(ns, max_split));
+    nitems = nst * nsplit;
+    per_xcd = (nitems + 7) / 8;
+    grid = nitems;
+    rgrid = (int)std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ncu, (n_pad + 255) / 256));
+    const int64_t need_gp = (int64_t)nitems * wstride;
+    if (need_gp > gp_cap) {
+      if (dgp) HIPCHK(hipFree(dgp));
+      dgp = nullptr;
+      HIPCHK(hipMalloc(&dgp, sizeof(double) * need_gp));
+      gp_cap = need_gp;
+    }
+    const int64_t need_rp = (int64_t)rgrid * NS;
+    if (need_rp > rp_cap) {
+      if (drp) HIPCHK(hipFree(drp));
+      drp = nullptr;
+      HIPCHK(hipMalloc(&drp, sizeof(double) * need_rp));
+      rp_cap = need_rp;
+    }
+    if (!evm) HIPCHK(hipEventCreate(&evm));
+    return SGLM_OK;
+  }
+
   int ensure_workspace() {
-    P16 = pass_variant((int)p);
-    stride = pass_stride(P16);
-    const int64_t want_grid = (int64_t)ncu * pass_wg_per_cu(P16);
-    grid = (int)(nblocks < want_grid ? (nblocks > 0 ? nblocks : 1) : want_grid);
+    if (wide) {
+      P16 = 0;
+      int rc = ensure_wide_workspace();
+      if (rc) return rc;
+    }
+    if (!wide) P16 = pass_variant((int)p);
+    stride = wide ? 0 : pass_stride(P16);
+    if (!wide) {
+      const int64_t want_grid = (int64_t)ncu * pass_wg_per_cu(P16);
+      grid = (int)(nblocks < want_grid ? (nblocks > 0 ? nblocks : 1) : want_grid);
+    }
     const int64_t need_part = std::max<int64_t>((int64_t)grid * stride, 4096 * NS);
     if (need_part > part_cap) {
       if (dpart) HIPCHK(hipFree(dpart));
@@ -169,7 +228,7 @@ struct sglm_engine : public Backend {
       HIPCHK(hipMalloc(&dpart, sizeof(double) * need_part));
       part_cap = need_part;
     }
-    const int64_t need_red = packed_len(p) + 16 * P16;
+    const int64_t need_red = packed_len(p) + 16 * std::max(P16, 1);
     if (need_red > red_cap) {
       if (dred) HIPCHK(hipFree(dred));
       if (dbeta) HIPCHK(hipFree(dbeta));
@@ -193,12 +252,13 @@ struct sglm_engine : public Backend {
       set_error("requirement failed: n >= 0 and p >= 1");
       return SGLM_EINVAL;
     }
-    if (p_ > 16 * MAX_P16) {
-      set_error("requirement failed: p <= 256 in this engine build (wide-p panels not yet enabled)");
+    if (p_ > MAX_P_WIDE) {
+      set_error("requirement failed: p <= " + std::to_string(MAX_P_WIDE) + " columns");
       return SGLM_EINVAL;
     }
     n = n_;
     p = p_;
+    wide = force_wide || p > 16 * MAX_P16;
     nblocks = (n + RB - 1) / RB;
     n_pad = std::max<int64_t>(nblocks, 1) * RB;
     const size_t vb = sizeof(double) * (size_t)n_pad;
@@ -211,7 +271,8 @@ struct sglm_engine : public Backend {
     }
     HIPCHK(hipMemsetAsync(dX, 0, vb * ncols, st));
     for (auto pr : {std::make_pair(&dy, true), std::make_pair(&dm, has_m), std::make_pair(&doff, has_off),
-                    std::make_pair(&dprior, has_prior), std::make_pair(&deta, true)}) {
+                    std::make_pair(&dprior, has_prior), std::make_pair(&deta, true), std::make_pair(&dw, wide),
+                    std::make_pair(&dwz, wide)}) {
       if (!pr.second) continue;
       e = hipMalloc(pr.first, vb);
       if (e != hipSuccess) {
@@ -272,13 +333,55 @@ struct sglm_engine : public Backend {
     a.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
-    if (nblocks > 0) {
-      HIPCHK(launch_pass(P16, a, grid, st));
+    if (wide) {
+      WideRowArgs r{};
+      r.X = dX;
+      r.ld = n_pad;
+      r.p = (int)p;
+      r.y = dy;
+      r.m = dm;
+      r.off = doff;
+      r.prior = dprior;
+      r.beta = beta ? dbeta : nullptr;
+      r.n = n;
+      r.n_pad = n_pad;
+      r.family = family;
+      r.link = link;
+      r.mode = mode;
+      r.mu0 = mu0;
+      r.ybar = ybar;
+      r.w = dw;
+      r.wz = dwz;
+      r.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
+      r.row_partials = drp;
+      HIPCHK(launch_wide_rows(r, rgrid, st));
+      HIPCHK(hipEventRecord(evm, st));
+      WideGramArgs g{};
+      g.X = dX;
+      g.ld = n_pad;
+      g.nq = (int)((p + 3) / 4);
+      g.w = dw;
+      g.wz = dwz;
+      g.nblocks = nblocks;
+      g.npan = npan;
+      g.nst = nst;
+      g.nsplit = nsplit;
+      g.nitems = nitems;
+      g.per_xcd = per_xcd;
+      g.partials = dgp;
+      g.stride = wstride;
+      HIPCHK(launch_wide_gram(g, st));
+      HIPCHK(hipEventRecord(ev1, st));
+      HIPCHK(launch_wide_reduce(dgp, wstride, nsplit, (int)p, drp, rgrid, dred, st));
     } else {
-      HIPCHK(hipMemsetAsync(dpart, 0, sizeof(double) * stride, st));
+      if (nblocks > 0) {
+        HIPCHK(launch_pass(P16, a, grid, st));
+      } else {
+        HIPCHK(hipMemsetAsync(dpart, 0, sizeof(double) * stride, st));
+      }
+      HIPCHK(hipEventRecord(ev1, st));
+      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st));
     }
-    HIPCHK(hipEventRecord(ev1, st));
-    HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st));
     HIPCHK(hipEventRecord(ev2, st));
     int rc = SGLM_OK;
     if (comm_on_device()) {
@@ -290,15 +393,38 @@ struct sglm_engine : public Backend {
     float k1 = 0.f, k2 = 0.f;
     HIPCHK(hipEventElapsedTime(&k1, ev0, ev1));
     HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
+    if (wide) {
+      float km = 0.f;
+      HIPCHK(hipEventElapsedTime(&km, ev0, evm));
+      row_ms += km;
+      gram_ms += k1 - km;
+    }
     passes += 1;
     pass_ms += k1;
     reduce_ms += k2;
     last_pass_ms = k1;
+    red_on_device = comm_on_device() || comm.kind == 0;
     if (!comm_on_device()) {
       rc = allreduce_host(hred, plen);
       if (rc) return rc;
     }
     std::memcpy(packed, hred, sizeof(double) * plen);
+    return SGLM_OK;
+  }
+
+  std::unique_ptr<SolverIface> make_solver(int64_t pp) override;
+  int blas_handle() {
+    if (!blas) {
+      if (rocblas_create_handle(&blas) != rocblas_status_success) {
+        blas = nullptr;
+        set_error("rocblas_create_handle failed");
+        return SGLM_EHIP;
+      }
+    }
+    if (rocblas_set_stream(blas, st) != rocblas_status_success) {
+      set_error("rocblas_set_stream failed");
+      return SGLM_EHIP;
+    }
     return SGLM_OK;
   }
 
@@ -334,6 +460,117 @@ struct sglm_engine : public Backend {
     return allreduce_small(s, NS);
   }
 };
+
+// =====================================================================================
+// Device solver for wide p: Cholesky on the GPU from the reduced buffer.
+// A matrix potrf rejects (not positive definite) is handed to the host solver, whose LU
+// fallback keeps Breeze inv()'s semantics, exactly as on the narrow path.
+// =====================================================================================
+namespace {
+
+struct DeviceSolver : public SolverIface {
+  sglm_engine* e;
+  int64_t p;
+  double *dA = nullptr, *dB = nullptr, *dAi = nullptr, *dpk = nullptr;
+  rocblas_int* dinfo = nullptr;
+  std::unique_ptr<HostSolver> host;
+  bool on_host = false, have_factor = false;
+  DeviceSolver(sglm_engine* eng, int64_t pp) : e(eng), p(pp) {}
+  ~DeviceSolver() override {
+    (void)hipSetDevice(e->device);
+    for (double* ptr : {dA, dB, dAi, dpk})
+      if (ptr) (void)hipFree(ptr);
+    if (dinfo) (void)hipFree(dinfo);
+  }
+  int alloc() {
+    if (dA) return SGLM_OK;
+    HIPCHK(hipMalloc(&dA, sizeof(double) * (size_t)(p * p)));
+    HIPCHK(hipMalloc(&dAi, sizeof(double) * (size_t)(p * p)));
+    HIPCHK(hipMalloc(&dB, sizeof(double) * (size_t)p));
+    HIPCHK(hipMalloc(&dinfo, sizeof(rocblas_int)));
+    return SGLM_OK;
+  }
+  int solve(const double* packed, double* x) override {
+    HIPCHK(hipSetDevice(e->device));
+    int rc = alloc();
+    if (!rc) rc = e->blas_handle();
+    if (rc) return rc;
+    const double* src = e->dred;
+    if (!e->red_on_device) {  // the reduction ended on the host: upload it
+      if (!dpk) HIPCHK(hipMalloc(&dpk, sizeof(double) * (size_t)packed_len(p)));
+      HIPCHK(hipMemcpyAsync(dpk, packed, sizeof(double) * (size_t)packed_len(p), hipMemcpyHostToDevice, e->st));
+      src = dpk;
+    }
+    HIPCHK(launch_unpack_lower(src, (int)p, dA, dB, e->st));
+    if (rocsolver_dpotrf(e->blas, rocblas_fill_lower, (rocblas_int)p, dA, (rocblas_int)p, dinfo) !=
+        rocblas_status_success) {
+      set_error("rocsolver_dpotrf failed");
+      return SGLM_EHIP;
+    }
+    rocblas_int info = 0;
+    HIPCHK(hipMemcpyAsync(&info, dinfo, sizeof info, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (info != 0) {
+      on_host = true;
+      have_factor = false;
+      if (!host) host = std::make_unique<HostSolver>(p);
+      return host->solve(packed, x);
+    }
+    if (rocsolver_dpotrs(e->blas, rocblas_fill_lower, (rocblas_int)p, 1, dA, (rocblas_int)p, dB, (rocblas_int)p) !=
+        rocblas_status_success) {
+      set_error("rocsolver_dpotrs failed");
+      return SGLM_EHIP;
+    }
+    HIPCHK(hipMemcpyAsync(x, dB, sizeof(double) * (size_t)p, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    on_host = false;
+    have_factor = true;
+    return SGLM_OK;
+  }
+  // inv(A) (lower triangle) into dAi from the kept factor
+  int device_inverse() {
+    HIPCHK(hipMemcpyAsync(dAi, dA, sizeof(double) * (size_t)(p * p), hipMemcpyDeviceToDevice, e->st));
+    if (rocsolver_dpotri(e->blas, rocblas_fill_lower, (rocblas_int)p, dAi, (rocblas_int)p, dinfo) !=
+        rocblas_status_success) {
+      set_error("rocsolver_dpotri failed");
+      return SGLM_EHIP;
+    }
+    return SGLM_OK;
+  }
+  int inv_diag(double* d) override {
+    if (on_host) return host->inv_diag(d);
+    if (!have_factor) {
+      for (int64_t i = 0; i < p; ++i) d[i] = 0.0;
+      return SGLM_OK;
+    }
+    HIPCHK(hipSetDevice(e->device));
+    int rc = device_inverse();
+    if (rc) return rc;
+    HIPCHK(hipMemcpy2DAsync(d, sizeof(double), dAi, sizeof(double) * (size_t)(p + 1), sizeof(double), (size_t)p,
+                            hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    return SGLM_OK;
+  }
+  int inverse(double* Ainv) override {
+    if (on_host) return host->inverse(Ainv);
+    if (!have_factor) return SGLM_OK;
+    HIPCHK(hipSetDevice(e->device));
+    int rc = device_inverse();
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(Ainv, dAi, sizeof(double) * (size_t)(p * p), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    for (int64_t j = 0; j < p; ++j)
+      for (int64_t i = 0; i < j; ++i) Ainv[i + j * p] = Ainv[j + i * p];
+    return SGLM_OK;
+  }
+};
+
+}  // namespace
+
+std::unique_ptr<SolverIface> sglm_engine::make_solver(int64_t pp) {
+  if (wide) return std::make_unique<DeviceSolver>(this, pp);
+  return std::make_unique<HostSolver>(pp);
+}
 
 // =====================================================================================
 // External backend adapter (caller-computed partials)
@@ -446,6 +683,7 @@ int sglm_create(int device, sglm_engine** out) {
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e, "hipGetDeviceProperties");
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char* ab = std::getenv("SGLM_DEBUG_ABLATE")) h->dbg = std::atoi(ab);
+  if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   *out = h;
   return SGLM_OK;
 }
@@ -652,13 +890,17 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->p = h->p;
   out->workgroups = h->grid;
   out->kernel_variant = h->P16;
+  out->path = h->wide ? 1 : 0;
+  out->wide_panels = h->wide ? h->npan : 0;
+  out->row_kernel_ms = h->row_ms;
+  out->gram_kernel_ms = h->wide ? h->gram_ms : h->pass_ms;
   return SGLM_OK;
 }
 
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   h->passes = 0;
-  h->pass_ms = h->reduce_ms = h->last_pass_ms = 0.0;
+  h->pass_ms = h->reduce_ms = h->last_pass_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;
   return SGLM_OK;

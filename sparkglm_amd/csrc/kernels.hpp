@@ -21,4 +21,13 @@ hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hip
 hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,
                         double* y, double* m, double* off, double* prior, hipStream_t st);
 
+// wide path (wide.hip)
+int wide_panels(int p);
+int64_t wide_stride();
+hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st);
+hipError_t launch_wide_gram(const WideGramArgs& a, hipStream_t st);
+hipError_t launch_wide_reduce(const double* part, int64_t stride, int nsplit, int p, const double* rowpart, int nrow,
+                              double* out, hipStream_t st);
+hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st);
+
 }  // namespace sglm

@@ -1,0 +1,405 @@
+// wide.hip -- the wide-design (p > 256) IRLS pass for gfx950.
+//
+// A p x p Gramian no longer fits in one workgroup's registers beyond p = 256 (the fused
+// kernel keeps all 136 tiles of a 256-column Gram resident), so the pass splits in two
+// streaming kernels plus a fixed-order reduction:
+//
+//   wide_rows_kernel   eta = X beta + offset (etaCreate, GLM.scala:321-332), mu, g', V,
+//                      w and w*z (zwCreateBinomial, GLM.scala:359-395) and the deviance
+//                      partials; one coalesced read of X (thread per row), w / w*z
+//                      written to two n-vectors.                       -> HBM-bound
+//   wide_gram_kernel   X'WX over 128 x 128 column "super-tiles" (panel pairs I >= J) of
+//                      16x16 fp64 MFMA tiles, each workgroup one (super-tile, row range)
+//                      work item; diagonal super-tiles also form X'Wz.  Panels stream
+//                      through LDS by LDS-DMA, double-buffered.        -> MFMA-bound
+//   wide_reduce_kernel fixed-order sum of the work-item partials and the row partials
+//                      into the packed wire format (deterministic).
+//
+// (partitionComponents / wlsComponents, utils.scala:84-126.)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "rowmath.hpp"
+
+namespace sglm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace {
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left open (gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS image (doubles).  One 32-row block of one 128-column panel: column c at c*32, row r
+// in slot r ^ (2c & 31) (the fused kernel's conflict-free swizzle, applied on the source).
+constexpr int PANEL = WIDE_PANEL;          // columns per panel
+constexpr int PT = PANEL / 16;             // 16-column tile blocks per panel (8)
+constexpr int PB = PANEL * RB;             // doubles per panel block image (4096)
+constexpr int OFF_X = 0;                   // [2 buffers][2 panels (I, J)][PB]
+constexpr int OFF_V = 4 * PB;              // [2 buffers][w, w*z][RB]
+constexpr int LDS_DOUBLES = OFF_V + 4 * RB;
+constexpr int NWAVE = 8;
+
+// Stage block blk of panels I (and J unless DIAG) into buffer buf.  Every wave issues the
+// same number of DMA instructions (QW + 1), so one vmcnt immediate serves all waves.
+template <bool DIAG>
+__device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs& a, int64_t blk, int I, int J, int wv,
+                                       int lane) {
+  constexpr int QW = DIAG ? 4 : 8;  // column quads per wave
+  const int64_t r0 = blk * RB;
+  const int i = lane & 15, cq = lane >> 4;
+  const double* lbase = a.X + (int64_t)cq * a.ld + r0;
+#pragma unroll
+  for (int k = 0; k < QW; ++k) {
+    const int qq = wv * QW + k;  // 0..31 panel I, 32..63 panel J
+    const int ps = qq >> 5, ql = qq & 31;
+    const int q = (ps ? J : I) * (PANEL / 4) + ql;
+    const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
+    const int srow = (2 * i) ^ ((8 * ql + 2 * cq) & 31);
+    const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ql * 128), 16,
+                                     0, 0);
+  }
+  const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
+  const double* vsrc = (v ? a.wz : a.w) + r0 + 2 * lane;
+  if (lane < 16)
+    __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * RB), 16, 0, 0);
+}
+
+// Off-diagonal super-tile: wave wv owns tile rows 2(wv>>1)+{0,1} of panel I and tile
+// columns 4(wv&1)+{0..3} of panel J (8 tiles).  A = X_I * w (row-scaled), B = X_J.
+__device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[8]) {
+  const int cl = lane & 15, rq = lane >> 4;
+  const int tr0 = 2 * (wv >> 1), tc0 = 4 * (wv & 1);
+  const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * 32 + 512 * tr0;
+  const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * 32 + 512 * tc0;
+  const double* w = lds + OFF_V + (buf * 2 + 0) * RB;
+#pragma unroll 2
+  for (int s = 0; s < RB / 4; ++s) {
+    const int r = 4 * s + rq;
+    const int o = r ^ (2 * cl);
+    const double wr = w[r];
+    const double a0 = xI[o] * wr, a1 = xI[o + 512] * wr;
+    double b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[u] = xJ[o + 512 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b[u], acc[u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[4 + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b[u], acc[4 + u], 0, 0, 0);
+  }
+}
+
+// Diagonal super-tile: waves q and q+4 own tile rows LO = q and HI = 7-q (tiles (LO,0..LO)
+// and (HI,0..HI): 9 tiles); wave q runs k-steps 0-3 of each block, wave q+4 k-steps 4-7.
+template <int Q>
+__device__ __forceinline__ void diag_block(const double* lds, int buf, int lane, int s0, d4 (&acc)[9], double& xz_lo,
+                                           double& xz_hi) {
+  constexpr int LO = Q, HI = PT - 1 - Q;
+  const int cl = lane & 15, rq = lane >> 4;
+  const double* xs = lds + OFF_X + (buf * 2 + 0) * PB + cl * 32;
+  const double* w = lds + OFF_V + (buf * 2 + 0) * RB;
+  const double* wz = lds + OFF_V + (buf * 2 + 1) * RB;
+#pragma unroll 1
+  for (int s = s0; s < s0 + RB / 8; ++s) {
+    const int r = 4 * s + rq;
+    const int o = r ^ (2 * cl);
+    const double wr = w[r], wzr = wz[r];
+    const double x_lo = xs[o + 512 * LO], x_hi = xs[o + 512 * HI];
+    const double a_lo = x_lo * wr, a_hi = x_hi * wr;
+    xz_lo += x_lo * wzr;
+    xz_hi += x_hi * wzr;
+#pragma unroll
+    for (int k = 0; k <= PT; ++k) {
+      const double b = xs[o + 512 * (k <= LO ? k : k - LO - 1)];
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
+    }
+  }
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void wait_blk(bool next_in_flight) {
+  if (next_in_flight) {
+    wait_vm<(DIAG ? 4 : 8) + 1>();
+  } else {
+    wait_vm<0>();
+  }
+}
+
+template <int Q>
+__device__ void diag_item(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int wv, int lane,
+                          double* out) {
+  d4 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  double xz_lo = 0.0, xz_hi = 0.0;
+  const int s0 = (wv >> 2) * (RB / 8);
+  wstage<true>(lds, 0, a, b0, I, I, wv, lane);
+  if (b0 + 1 < b1) wstage<true>(lds, 1, a, b0 + 1, I, I, wv, lane);
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; ++blk) {
+    const int cur = (int)((blk - b0) & 1);
+    wait_blk<true>(blk + 1 < b1);
+    lds_bar();
+    diag_block<Q>(lds, cur, lane, s0, acc, xz_lo, xz_hi);
+    lds_bar();
+    if (blk + 2 < b1) wstage<true>(lds, cur, a, blk + 2, I, I, wv, lane);
+  }
+  // combine the two k-halves (wave q+4 -> LDS -> wave q), fixed order
+  constexpr int LO = Q, HI = PT - 1 - Q;
+  xz_lo += __shfl_xor(xz_lo, 16);
+  xz_lo += __shfl_xor(xz_lo, 32);
+  xz_hi += __shfl_xor(xz_hi, 16);
+  xz_hi += __shfl_xor(xz_hi, 32);
+  double* scr = lds + OFF_X + Q * (9 * 256 + 32);
+  if (wv >= 4) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) scr[k * 256 + 64 * j + lane] = acc[k][j];
+    if (lane < 16) {
+      scr[9 * 256 + lane] = xz_lo;
+      scr[9 * 256 + 16 + lane] = xz_hi;
+    }
+  }
+  lds_bar();
+  if (wv < 4) {
+#pragma unroll
+    for (int k = 0; k <= PT; ++k) {
+      const int bi = k <= LO ? LO : HI, bj = k <= LO ? k : k - LO - 1;
+      const int t = bi * PT + bj;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j] + scr[k * 256 + 64 * j + lane];
+    }
+    if (lane < 16) {
+      out[PT * PT * 256 + 16 * LO + lane] = xz_lo + scr[9 * 256 + lane];
+      out[PT * PT * 256 + 16 * HI + lane] = xz_hi + scr[9 * 256 + 16 + lane];
+    }
+  }
+}
+
+__device__ void offdiag_item(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int wv,
+                             int lane, double* out) {
+  d4 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  wstage<false>(lds, 0, a, b0, I, J, wv, lane);
+  if (b0 + 1 < b1) wstage<false>(lds, 1, a, b0 + 1, I, J, wv, lane);
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; ++blk) {
+    const int cur = (int)((blk - b0) & 1);
+    wait_blk<false>(blk + 1 < b1);
+    lds_bar();
+    offdiag_block(lds, cur, wv, lane, acc);
+    lds_bar();
+    if (blk + 2 < b1) wstage<false>(lds, cur, a, blk + 2, I, J, wv, lane);
+  }
+  const int tr0 = 2 * (wv >> 1), tc0 = 4 * (wv & 1);
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = (tr0 + t2) * PT + tc0 + u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t2 * 4 + u][j];
+    }
+}
+
+}  // namespace
+
+// Work item it = (super-tile st, row split s), st = I(I+1)/2 + J.  Workgroup b runs on XCD
+// b % 8; items are dealt to XCDs in contiguous ranges so that the concurrently running
+// super-tiles of one row split share that XCD's L2.
+__global__ void __launch_bounds__(64 * NWAVE, 1) wide_gram_kernel(WideGramArgs a) {
+  __shared__ double lds[LDS_DOUBLES];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int it = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  if (it >= a.nitems) return;
+  const int s = it / a.nst, st = it - s * a.nst;
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= st) ++I;
+  const int J = st - I * (I + 1) / 2;
+  const int64_t b0 = (a.nblocks * s) / a.nsplit, b1 = (a.nblocks * (s + 1)) / a.nsplit;
+  double* out = a.partials + ((int64_t)st * a.nsplit + s) * a.stride;
+  if (b0 >= b1) {  // empty row range: zero partial
+    for (int e = threadIdx.x; e < a.stride; e += 64 * NWAVE) out[e] = 0.0;
+    return;
+  }
+  if (I != J) {
+    offdiag_item(lds, a, I, J, b0, b1, wv, lane, out);
+  } else {
+    switch (wv & 3) {
+      case 0: diag_item<0>(lds, a, I, b0, b1, wv, lane, out); break;
+      case 1: diag_item<1>(lds, a, I, b0, b1, wv, lane, out); break;
+      case 2: diag_item<2>(lds, a, I, b0, b1, wv, lane, out); break;
+      default: diag_item<3>(lds, a, I, b0, b1, wv, lane, out); break;
+    }
+  }
+}
+
+// Row stage: thread per row, columns streamed in order with four partial sums.
+template <int FAM, int LNK>
+__global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
+  __shared__ double red[4][2];
+  const int64_t per = (a.n_pad + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = (lo + per < a.n_pad) ? lo + per : a.n_pad;
+  double s_dev = 0.0, s_aux = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    double eta = 0.0;
+    if (a.mode == MODE_IRLS) {
+      double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
+      const double* xc = a.X + i;
+      int j = 0;
+#pragma unroll 2
+      for (; j + 4 <= a.p; j += 4) {
+        e0 += xc[(int64_t)j * a.ld] * a.beta[j];
+        e1 += xc[(int64_t)(j + 1) * a.ld] * a.beta[j + 1];
+        e2 += xc[(int64_t)(j + 2) * a.ld] * a.beta[j + 2];
+        e3 += xc[(int64_t)(j + 3) * a.ld] * a.beta[j + 3];
+      }
+      for (; j < a.p; ++j) e0 += xc[(int64_t)j * a.ld] * a.beta[j];
+      eta = (e0 + e1) + (e2 + e3);
+    }
+    double w = 0.0, wz = 0.0;
+    if (i < a.n) {
+      const double y = a.y[i];
+      const double m = a.m ? a.m[i] : 1.0;
+      const double off = a.off ? a.off[i] : 0.0;
+      const double pw = a.prior ? a.prior[i] : 1.0;
+      if (a.mode == MODE_IRLS) {
+        eta = eta + off;
+        if (a.eta_out) a.eta_out[i] = eta;
+      }
+      pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
+    }
+    a.w[i] = w;
+    a.wz[i] = wz;
+  }
+  for (int o = 1; o < 64; o <<= 1) {
+    s_dev += __shfl_xor(s_dev, o);
+    s_aux += __shfl_xor(s_aux, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6][0] = s_dev;
+    red[threadIdx.x >> 6][1] = s_aux;
+  }
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    const int k = threadIdx.x;
+    double v = 0.0;
+    if (k == S_DEV) v = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+    if (k == S_SUMW) v = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+    a.row_partials[(int64_t)blockIdx.x * NS + k] = v;
+  }
+}
+
+// Packed output: lower-tri X'WX row-major | X'Wz | NS scalars, summed in a fixed order.
+__global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stride, int nsplit, int p,
+                                   const double* __restrict__ rowpart, int nrow, double* __restrict__ out) {
+  const int64_t tri = (int64_t)p * (p + 1) / 2;
+  const int64_t total = tri + p + NS;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    if (e < tri + p) {
+      int64_t st, src;
+      if (e < tri) {
+        int64_t i = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+        while (i * (i + 1) / 2 > e) --i;
+        while ((i + 1) * (i + 2) / 2 <= e) ++i;
+        const int64_t j = e - i * (i + 1) / 2;
+        const int64_t I = i / PANEL, J = j / PANEL;
+        st = I * (I + 1) / 2 + J;
+        src = (((i % PANEL) >> 4) * PT + ((j % PANEL) >> 4)) * 256 + (i & 15) * 16 + (j & 15);
+      } else {
+        const int64_t c = e - tri, I = c / PANEL;
+        st = I * (I + 1) / 2 + I;
+        src = PT * PT * 256 + (c % PANEL);
+      }
+      const double* ps = part + st * nsplit * stride + src;
+      for (int g = 0; g < nsplit; ++g) s += ps[(int64_t)g * stride];
+    } else {
+      const int k = (int)(e - tri - p);
+      for (int g = 0; g < nrow; ++g) s += rowpart[(int64_t)g * NS + k];
+    }
+    out[e] = s;
+  }
+}
+
+// Packed lower triangle (row-major) -> column-major p x p lower triangle (for potrf) and X'Wz.
+__global__ void unpack_lower_kernel(const double* __restrict__ packed, int p, double* __restrict__ A,
+                                    double* __restrict__ b) {
+  const int64_t tri = (int64_t)p * (p + 1) / 2;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tri + p; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < tri) {
+      int64_t i = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+      while (i * (i + 1) / 2 > e) --i;
+      while ((i + 1) * (i + 2) / 2 <= e) ++i;
+      const int64_t j = e - i * (i + 1) / 2;
+      A[i + j * (int64_t)p] = packed[e];
+    } else {
+      b[e - tri] = packed[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------
+int wide_panels(int p) { return (p + PANEL - 1) / PANEL; }
+int64_t wide_stride() { return (int64_t)PT * PT * 256 + PANEL; }
+
+hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st) {
+  const dim3 g(grid), b(256);
+  const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
+  const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
+  else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, a);
+  else if (fam == FAM_BINOMIAL)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, a);
+  else if (fam == FAM_GAUSSIAN)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, a);
+  else if (fam == FAM_POISSON)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_POISSON, LNK_LOG>), g, b, 0, st, a);
+  else if (fam == FAM_GAMMA)
+    hipLaunchKernelGGL((wide_rows_kernel<FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_gram(const WideGramArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(wide_gram_kernel, dim3(8 * a.per_xcd), dim3(64 * NWAVE), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_reduce(const double* part, int64_t stride, int nsplit, int p, const double* rowpart, int nrow,
+                              double* out, hipStream_t st) {
+  const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, stride, nsplit, p, rowpart, nrow, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st) {
+  const int64_t total = (int64_t)p * (p + 1) / 2 + p;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(unpack_lower_kernel, dim3(blocks), dim3(256), 0, st, packed, p, A, b);
+  return hipGetLastError();
+}
+
+}  // namespace sglm

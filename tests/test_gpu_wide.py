@@ -1,0 +1,179 @@
+"""Parity of the wide-design path (wide.hip: row kernel + panel-pair Gram kernel + rocSOLVER
+solve) against the oracle.
+
+The path runs natively for p > 256; SGLM_FORCE_WIDE=1 (read when an engine is created)
+routes small designs through it too, so every golden case and the panel-edge shapes are
+covered.  Bar as everywhere: coefficients / standard errors / deviance within 1e-9
+relative, same iteration count; Gramians norm-wise within 1e-13."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from conftest import nrel, rel
+from sparkglm_amd import Engine, synth
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def weng():
+    old = os.environ.get("SGLM_FORCE_WIDE")
+    os.environ["SGLM_FORCE_WIDE"] = "1"
+    try:
+        e = Engine(0)
+    finally:
+        if old is None:
+            del os.environ["SGLM_FORCE_WIDE"]
+        else:
+            os.environ["SGLM_FORCE_WIDE"] = old
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _logit_pass_check(e, X, y, beta):
+    G, xz, s = e.irls_pass(beta)
+    eta = X @ beta
+    mu = 1 / (1 + np.exp(-eta))
+    w = mu * (1 - mu)
+    z = eta + (y - mu) / w
+    assert nrel(G, (X * w[:, None]).T @ X) < 1e-13
+    assert nrel(xz, X.T @ (w * z)) < 1e-13
+    dev = np.sum(y * np.log(np.maximum(y, 1) / mu) + (1 - y) * np.log(np.maximum(1 - y, 1) / (1 - mu)))
+    assert rel(s[0], dev) < 1e-12
+    return G
+
+
+@pytest.mark.parametrize("p", [1, 2, 17, 64, 127, 128, 129, 200, 256])
+def test_forced_wide_gram(weng, p):
+    rng = np.random.default_rng(p)
+    n = 3000 + 7 * p
+    X = rng.uniform(-1, 1, (n, p))
+    X[:, 0] = 1.0
+    y = (rng.uniform(size=n) < 0.4).astype(float)
+    weng.set_data(X, y)
+    _logit_pass_check(weng, X, y, rng.normal(size=p) * 0.2)
+    st = weng.stats()
+    assert st["path"] == 1 and st["wide_panels"] == (p + 127) // 128
+
+
+@pytest.mark.parametrize("p", [257, 300, 384, 520, 1030])
+def test_native_wide_gram(eng, p):
+    rng = np.random.default_rng(p)
+    n = 3000 + 7 * p
+    X = rng.uniform(-1, 1, (n, p)) / np.sqrt(p)
+    X[:, 0] = 1.0
+    y = (rng.uniform(size=n) < 0.4).astype(float)
+    eng.set_data(X, y)
+    _logit_pass_check(eng, X, y, rng.normal(size=p) * 0.5)
+    assert eng.stats()["path"] == 1
+
+
+def test_forced_wide_golden_cases(weng, golden):
+    for name, c in golden.items():
+        fam, link, npart = (str(v) for v in c["meta"])
+        weng.set_data(c["X"], c["y"], c.get("m"), c.get("offset"), c.get("prior"))
+        f = weng.fit_glm(fam, link, init="multiple" if npart != "1" else "single")
+        s = c["scalars"]
+        assert f.iter == int(s[4]), name
+        if np.isnan(s[0]):
+            assert np.isnan(f.deviance), name
+            continue
+        assert rel(f.coefs, c["coefs"]) < TOL, name
+        assert rel(f.stderr, c["stderr"]) < TOL, name
+        assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik], s[:4]) < TOL, name
+        assert rel(f.dev_trace, c["trace"]) < TOL, name
+
+
+def test_forced_wide_edge_shapes(weng):
+    rng = np.random.default_rng(11)
+    for n, p in ((1, 1), (5, 1), (31, 2), (32, 3), (33, 3), (64, 16), (65, 130)):
+        X = rng.uniform(-1, 1, (n, p))
+        X[:, 0] = 1.0
+        y = rng.normal(size=n) + 3
+        weng.set_data(X, y)
+        G, xz, s = weng.irls_pass(np.zeros(p), family="gaussian", link="identity")
+        assert nrel(G, X.T @ X) < 1e-13 and nrel(xz, X.T @ y) < 1e-13
+        if n > p:
+            f = weng.fit_lm()
+            r = po.fit_lm(X, y)
+            assert rel(f.coefs, r["coefs"]) < TOL and rel(f.stderr, r["stderr"]) < TOL
+            assert rel(f.xtxi, r["xtxi"]) < 1e-8
+
+
+def _gamma_data(n, p, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0.5, 1.5, (n, p)) / p
+    X[:, 0] = 1.0
+    beta = np.full(p, 0.5)
+    mu = 1.0 / (X @ beta)
+    y = rng.gamma(5.0, mu / 5.0)
+    return X, y
+
+
+@pytest.mark.parametrize("case", ["logit300", "probit264", "poisson300", "gamma260", "cloglog520"])
+def test_native_wide_fits_match_oracle(eng, case):
+    kw = {}
+    if case == "logit300":
+        X, y, _, _ = synth.generate(0, 0, 15000, 300, 31)
+        fam, link = "binomial", "logit"
+    elif case == "probit264":
+        X, y, _, _ = synth.generate(0, 0, 12000, 264, 32)
+        fam, link = "binomial", "probit"
+    elif case == "poisson300":
+        X, y, off, pr = synth.generate(2, 0, 15000, 300, 33)
+        fam, link = "poisson", "log"
+        kw = dict(offset=off, prior=pr)
+    elif case == "gamma260":
+        X, y = _gamma_data(12000, 260, 34)
+        fam, link = "gamma", "inverse"
+    else:
+        X, y, _, _ = synth.generate(0, 0, 20000, 520, 35)
+        y = (synth.unif(np.arange(20000, dtype=np.uint64) + np.uint64(91)) < 0.3).astype(float)
+        fam, link = "binomial", "cloglog"
+    eng.set_data(X, y, offset=kw.get("offset"), prior=kw.get("prior"))
+    f = eng.fit_glm(fam, link)
+    o = po.fit_glm(X, y, fam, link, nthreads=8, **kw)
+    assert f.iter == o.iter, case
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL, case
+    assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
+               [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL, case
+
+
+def test_native_wide_lm(eng):
+    X, y, _, _ = synth.generate(1, 0, 20000, 300, 36)
+    eng.set_data(X, y)
+    f = eng.fit_lm()
+    r = po.fit_lm(X, y, nthreads=8)
+    assert rel(f.coefs, r["coefs"]) < TOL and rel(f.stderr, r["stderr"]) < TOL
+    assert rel([f.sse, f.r2, f.fstat, f.sigma], [r["sse"], r["r2"], r["fstat"], r["sigma"]]) < TOL
+
+
+def test_wide_large_properties(eng):
+    """1M x 512 resident logit fit: a 20k-row prefix against the oracle, then at full size the
+    score equation at the MLE, monotone deviance and bitwise run-to-run determinism."""
+    p = 512
+    eng.synth(0, 0, 20_000, p, 5)
+    X, y, _, _, _ = eng.get_data()
+    f = eng.fit_glm()
+    o = po.fit_glm(X, y, nthreads=8)
+    assert f.iter == o.iter and rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel(f.deviance, o.deviance) < TOL
+    del X, y
+    eng.synth(0, 0, 1_000_000, p, 5)
+    f = eng.fit_glm()
+    assert np.all(np.diff(f.dev_trace[: f.iter + 1]) <= 1e-6)
+    G, xz, _ = eng.irls_pass(f.coefs)
+    assert np.max(np.abs(xz - G @ f.coefs)) < 1e-6 * np.max(np.abs(xz))
+    g = eng.fit_glm()
+    np.testing.assert_array_equal(f.coefs, g.coefs)
+    np.testing.assert_array_equal(f.stderr, g.stderr)

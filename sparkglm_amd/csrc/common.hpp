@@ -72,19 +72,26 @@ struct WideRowArgs {
   double* row_partials; // [grid][NS]
 };
 
+// One run of consecutive 16-row blocks of one super-tile, processed by one workgroup of
+// the persistent Gram kernel and written to partial slot `slot`.
+struct WidePiece {
+  int64_t b0, b1;       // [b0, b1) blocks of WIDE_RB rows
+  int st;               // super-tile I(I+1)/2 + J
+  int slot;             // partial slot (slots of one super-tile are consecutive)
+};
+constexpr int WIDE_RB = 16;   // rows per Gram-kernel LDS block
+
 struct WideGramArgs {
   const double* X;
   int64_t ld;
-  int nq;               // column quads stored
+  int ncols;            // columns stored (multiple of 4, zero past p)
   const double* w;
   const double* wz;
-  int64_t nblocks;      // row blocks of RB rows
-  int npan, nst;        // panels, super-tiles npan(npan+1)/2
-  int nsplit;           // row splits per super-tile
-  int nitems;           // nst * nsplit
-  int per_xcd;          // items per XCD (grid = 8 * per_xcd)
-  double* partials;     // [nst][nsplit][stride]
+  const WidePiece* pieces;
+  const int* wg_begin;  // [grid + 1]: pieces of workgroup g are [wg_begin[g], wg_begin[g+1])
+  double* partials;     // [slots][stride]
   int64_t stride;
+  int dbg;              // profiling ablations: 4 DMA, 32 barriers
 };
 
 // Arguments of the final-statistics pass (stats_kernel).

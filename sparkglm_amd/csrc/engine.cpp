@@ -85,7 +85,11 @@ struct sglm_engine : public Backend {
   bool wide = false, force_wide = false;
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
-  int npan = 0, nst = 0, nsplit = 0, nitems = 0, per_xcd = 0, rgrid = 0;
+  int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
+  WidePiece* dpieces[2] = {nullptr, nullptr};  // [0] off-diagonal, [1] diagonal super-tiles
+  int* dwgb[2] = {nullptr, nullptr};
+  int* dstr = nullptr;                          // [nst][2] partial slot range per super-tile
+  bool has_sched[2] = {false, false};
   hipEvent_t evm = nullptr;
   rocblas_handle blas = nullptr;
   // stats
@@ -109,6 +113,7 @@ struct sglm_engine : public Backend {
       if (*ptr) (void)hipFree(*ptr);
       *ptr = nullptr;
     }
+    free_schedule();
     part_cap = red_cap = gp_cap = rp_cap = 0;
     if (blas) (void)rocblas_destroy_handle(blas);
     blas = nullptr;
@@ -178,20 +183,78 @@ struct sglm_engine : public Backend {
     return allreduce_host(h, count);
   }
 
+  void free_schedule() {
+    for (int k = 0; k < 2; ++k) {
+      if (dpieces[k]) (void)hipFree(dpieces[k]);
+      if (dwgb[k]) (void)hipFree(dwgb[k]);
+      dpieces[k] = nullptr;
+      dwgb[k] = nullptr;
+      has_sched[k] = false;
+    }
+    if (dstr) (void)hipFree(dstr);
+    dstr = nullptr;
+  }
+
+  // Cost-balanced static schedules of the persistent Gram kernels.  For each kernel (off-
+  // diagonal / diagonal super-tiles) the (super-tile, block) line, super-tile major, is cut
+  // into ggrid equal segments; a segment's runs inside one super-tile are its pieces.
+  // Pieces are numbered in line order, so the partial slots of a super-tile are consecutive.
+  int build_wide_schedule() {
+    const int64_t nb = n_pad / WIDE_RB;
+    std::vector<int> str((size_t)nst * 2, 0);
+    free_schedule();
+    int slot = 0;
+    for (int kind = 0; kind < 2; ++kind) {
+      std::vector<int> sts;
+      for (int I = 0; I < npan; ++I)
+        for (int J = 0; J <= I; ++J)
+          if ((I == J) == (kind == 1)) sts.push_back(I * (I + 1) / 2 + J);
+      if (sts.empty()) continue;
+      const int64_t total = nb * (int64_t)sts.size();
+      std::vector<WidePiece> pieces;
+      std::vector<int> wgb((size_t)ggrid + 1, 0);
+      int64_t pos = 0, b = 0;
+      size_t si = 0;
+      for (int g = 0; g < ggrid; ++g) {
+        wgb[(size_t)g] = (int)pieces.size();
+        const int64_t end = (int64_t)((__int128)total * (g + 1) / ggrid);
+        while (si < sts.size() && pos < end) {
+          const int64_t k = std::min(nb - b, end - pos);
+          const int st = sts[si];
+          if (b == 0) str[(size_t)st * 2] = slot;
+          pieces.push_back(WidePiece{b, b + k, st, slot++});
+          str[(size_t)st * 2 + 1] = slot;
+          pos += k;
+          b += k;
+          if (b == nb) {
+            ++si;
+            b = 0;
+          }
+        }
+      }
+      wgb[(size_t)ggrid] = (int)pieces.size();
+      HIPCHK(hipMalloc(&dpieces[kind], sizeof(WidePiece) * pieces.size()));
+      HIPCHK(hipMalloc(&dwgb[kind], sizeof(int) * wgb.size()));
+      HIPCHK(hipMemcpy(dpieces[kind], pieces.data(), sizeof(WidePiece) * pieces.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(dwgb[kind], wgb.data(), sizeof(int) * wgb.size(), hipMemcpyHostToDevice));
+      has_sched[kind] = true;
+    }
+    nslots = slot;
+    HIPCHK(hipMalloc(&dstr, sizeof(int) * str.size()));
+    HIPCHK(hipMemcpy(dstr, str.data(), sizeof(int) * str.size(), hipMemcpyHostToDevice));
+    return SGLM_OK;
+  }
+
   int ensure_wide_workspace() {
     npan = wide_panels((int)p);
     nst = npan * (npan + 1) / 2;
     wstride = wide_stride();
-    // work items: ~8 per CU so the tail of unequal items stays short; >= 16 blocks each
-    const int64_t target = 8 * (int64_t)ncu;
-    int64_t ns = (target + nst - 1) / nst;
-    const int64_t max_split = std::max<int64_t>(1, nblocks / 16);
-    nsplit = (int)std::max<int64_t>(1, std::min(ns, max_split));
-    nitems = nst * nsplit;
-    per_xcd = (nitems + 7) / 8;
-    grid = nitems;
+    ggrid = ncu * wide_gram_wg_per_cu();
+    int rc = build_wide_schedule();
+    if (rc) return rc;
+    grid = nslots;
     rgrid = (int)std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ncu, (n_pad + 255) / 256));
-    const int64_t need_gp = (int64_t)nitems * wstride;
+    const int64_t need_gp = (int64_t)std::max(nslots, 1) * wstride;
     if (need_gp > gp_cap) {
       if (dgp) HIPCHK(hipFree(dgp));
       dgp = nullptr;
@@ -359,20 +422,20 @@ struct sglm_engine : public Backend {
       WideGramArgs g{};
       g.X = dX;
       g.ld = n_pad;
-      g.nq = (int)((p + 3) / 4);
+      g.ncols = (int)((p + 3) / 4 * 4);
       g.w = dw;
       g.wz = dwz;
-      g.nblocks = nblocks;
-      g.npan = npan;
-      g.nst = nst;
-      g.nsplit = nsplit;
-      g.nitems = nitems;
-      g.per_xcd = per_xcd;
       g.partials = dgp;
       g.stride = wstride;
-      HIPCHK(launch_wide_gram(g, st));
+      g.dbg = dbg;
+      for (int kind = 0; kind < 2; ++kind) {
+        if (!has_sched[kind]) continue;
+        g.pieces = dpieces[kind];
+        g.wg_begin = dwgb[kind];
+        HIPCHK(launch_wide_gram(g, kind == 1, ggrid, st));
+      }
       HIPCHK(hipEventRecord(ev1, st));
-      HIPCHK(launch_wide_reduce(dgp, wstride, nsplit, (int)p, drp, rgrid, dred, st));
+      HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dred, st));
     } else {
       if (nblocks > 0) {
         HIPCHK(launch_pass(P16, a, grid, st));

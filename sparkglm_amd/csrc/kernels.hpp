@@ -25,9 +25,10 @@ hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed,
 int wide_panels(int p);
 int64_t wide_stride();
 hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st);
-hipError_t launch_wide_gram(const WideGramArgs& a, hipStream_t st);
-hipError_t launch_wide_reduce(const double* part, int64_t stride, int nsplit, int p, const double* rowpart, int nrow,
-                              double* out, hipStream_t st);
+int wide_gram_wg_per_cu();
+hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st);
+hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,
+                              int nrow, double* out, hipStream_t st);
 hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st);
 
 }  // namespace sglm

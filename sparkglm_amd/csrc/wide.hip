@@ -9,8 +9,9 @@
 //                      partials; one coalesced read of X (thread per row), w / w*z
 //                      written to two n-vectors.                       -> HBM-bound
 //   wide_gram_kernel   X'WX over 128 x 128 column "super-tiles" (panel pairs I >= J) of
-//                      16x16 fp64 MFMA tiles, each workgroup one (super-tile, row range)
-//                      work item; diagonal super-tiles also form X'Wz.  Panels stream
+//                      16x16 fp64 MFMA tiles; persistent, two 4-wave workgroups per CU,
+//                      each running a cost-balanced list of (super-tile, row range)
+//                      pieces; diagonal super-tiles also form X'Wz.  Panels stream
 //                      through LDS by LDS-DMA, double-buffered.        -> MFMA-bound
 //   wide_reduce_kernel fixed-order sum of the work-item partials and the row partials
 //                      into the packed wire format (deterministic).
@@ -40,211 +41,197 @@ __device__ __forceinline__ void wait_vm() {
 
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// LDS image (doubles).  One 32-row block of one 128-column panel: column c at c*32, row r
-// in slot r ^ (2c & 31) (the fused kernel's conflict-free swizzle, applied on the source).
+// LDS image (doubles) of one 16-row block of one 128-column panel: column c at c*16, row r
+// in slot r ^ f(c), f(c) = 2((c >> 1) & 7).  The XOR is applied on the DMA source address
+// (the LDS-DMA destination is lane-linear; f even keeps each lane's 16-byte row pair
+// contiguous) and makes the MFMA fragment reads (ds_read_b64, lanes (rq, cl) reading row
+// 4s+rq of column 16b+cl) bank-conflict free: within each 32-lane group the 32 reads hit
+// 16*(cl & 1) + ((4s + rq) ^ 2(cl >> 1)) mod 32, all distinct.
 constexpr int PANEL = WIDE_PANEL;          // columns per panel
 constexpr int PT = PANEL / 16;             // 16-column tile blocks per panel (8)
-constexpr int PB = PANEL * RB;             // doubles per panel block image (4096)
+constexpr int WRB = WIDE_RB;               // rows per block (16)
+constexpr int PB = PANEL * WRB;            // doubles per panel block image (2048)
+constexpr int TB = 16 * WRB;               // doubles per 16-column tile block (256)
 constexpr int OFF_X = 0;                   // [2 buffers][2 panels (I, J)][PB]
-constexpr int OFF_V = 4 * PB;              // [2 buffers][w, w*z][RB]
-constexpr int LDS_DOUBLES = OFF_V + 4 * RB;
-constexpr int NWAVE = 8;
+constexpr int OFF_V = 4 * PB;              // [2 buffers][w, w*z][WRB]
+constexpr int LDS_DOUBLES = OFF_V + 4 * WRB;
+constexpr int NWAVE = 4;                   // one wave per SIMD; two workgroups per CU
 
-// Stage block blk of panels I (and J unless DIAG) into buffer buf.  Every wave issues the
-// same number of DMA instructions (QW + 1), so one vmcnt immediate serves all waves.
+__device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
+
+// Stage block blk of panels I (and J unless DIAG) into buffer buf: one global_load_lds of
+// 16 bytes per lane moves an "octet" of 8 columns x 16 rows; 16 octets per panel.
 template <bool DIAG>
 __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs& a, int64_t blk, int I, int J, int wv,
                                        int lane) {
-  constexpr int QW = DIAG ? 4 : 8;  // column quads per wave
-  const int64_t r0 = blk * RB;
-  const int i = lane & 15, cq = lane >> 4;
-  const double* lbase = a.X + (int64_t)cq * a.ld + r0;
+  constexpr int OW = DIAG ? 4 : 8;  // octets per wave
+  const int64_t r0 = blk * WRB;
+  const int i = lane & 7, oc = lane >> 3;
 #pragma unroll
-  for (int k = 0; k < QW; ++k) {
-    const int qq = wv * QW + k;  // 0..31 panel I, 32..63 panel J
-    const int ps = qq >> 5, ql = qq & 31;
-    const int q = (ps ? J : I) * (PANEL / 4) + ql;
-    const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
-    const int srow = (2 * i) ^ ((8 * ql + 2 * cq) & 31);
-    const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ql * 128), 16,
+  for (int k = 0; k < OW; ++k) {
+    const int qq = wv * OW + k;  // 0..15 panel I, 16..31 panel J
+    const int ps = qq >> 4, ol = qq & 15;
+    const int cp = ol * 8 + oc;                    // column within the panel
+    int gc = (ps ? J : I) * PANEL + cp;            // column of X
+    gc = gc < a.ncols ? gc : a.ncols - 1;          // columns past the stored ones: duplicates
+    const double* src = a.X + (int64_t)gc * a.ld + r0 + ((2 * i) ^ swz(cp));
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16,
                                      0, 0);
   }
   const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
   const double* vsrc = (v ? a.wz : a.w) + r0 + 2 * lane;
-  if (lane < 16)
-    __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * RB), 16, 0, 0);
+  if (lane < WRB / 2)
+    __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
 }
 
-// Off-diagonal super-tile: wave wv owns tile rows 2(wv>>1)+{0,1} of panel I and tile
-// columns 4(wv&1)+{0..3} of panel J (8 tiles).  A = X_I * w (row-scaled), B = X_J.
-__device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[8]) {
+// Off-diagonal super-tile: wave wv owns tile rows 4(wv>>1)+{0..3} of panel I and tile
+// columns 4(wv&1)+{0..3} of panel J (16 tiles).  A = X_I * w (row-scaled), B = X_J.
+__device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[16]) {
   const int cl = lane & 15, rq = lane >> 4;
-  const int tr0 = 2 * (wv >> 1), tc0 = 4 * (wv & 1);
-  const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * 32 + 512 * tr0;
-  const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * 32 + 512 * tc0;
-  const double* w = lds + OFF_V + (buf * 2 + 0) * RB;
+  const int f = 2 * (cl >> 1);
+  const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB + TB * (4 * (wv >> 1));
+  const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * WRB + TB * (4 * (wv & 1));
+  const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
 #pragma unroll 2
-  for (int s = 0; s < RB / 4; ++s) {
+  for (int s = 0; s < WRB / 4; ++s) {
     const int r = 4 * s + rq;
-    const int o = r ^ (2 * cl);
+    const int o = r ^ f;
     const double wr = w[r];
-    const double a0 = xI[o] * wr, a1 = xI[o + 512] * wr;
-    double b[4];
+    double av[4], bv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) b[u] = xJ[o + 512 * u];
+    for (int t = 0; t < 4; ++t) av[t] = xI[o + TB * t] * wr;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b[u], acc[u], 0, 0, 0);
+    for (int u = 0; u < 4; ++u) bv[u] = xJ[o + TB * u];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[4 + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b[u], acc[4 + u], 0, 0, 0);
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[4 * t + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[u], acc[4 * t + u], 0, 0, 0);
   }
 }
 
-// Diagonal super-tile: waves q and q+4 own tile rows LO = q and HI = 7-q (tiles (LO,0..LO)
-// and (HI,0..HI): 9 tiles); wave q runs k-steps 0-3 of each block, wave q+4 k-steps 4-7.
+// Diagonal super-tile: wave q owns tile rows LO = q and HI = 7-q of the lower tile grid,
+// tiles (LO,0..LO) and (HI,0..HI): 9 tiles, 36 over the four waves; X'Wz on the VALU.
 template <int Q>
-__device__ __forceinline__ void diag_block(const double* lds, int buf, int lane, int s0, d4 (&acc)[9], double& xz_lo,
+__device__ __forceinline__ void diag_block(const double* lds, int buf, int lane, d4 (&acc)[9], double& xz_lo,
                                            double& xz_hi) {
   constexpr int LO = Q, HI = PT - 1 - Q;
   const int cl = lane & 15, rq = lane >> 4;
-  const double* xs = lds + OFF_X + (buf * 2 + 0) * PB + cl * 32;
-  const double* w = lds + OFF_V + (buf * 2 + 0) * RB;
-  const double* wz = lds + OFF_V + (buf * 2 + 1) * RB;
-#pragma unroll 1
-  for (int s = s0; s < s0 + RB / 8; ++s) {
+  const int f = 2 * (cl >> 1);
+  const double* xs = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB;
+  const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
+  const double* wz = lds + OFF_V + (buf * 2 + 1) * WRB;
+#pragma unroll
+  for (int s = 0; s < WRB / 4; ++s) {
     const int r = 4 * s + rq;
-    const int o = r ^ (2 * cl);
+    const int o = r ^ f;
     const double wr = w[r], wzr = wz[r];
-    const double x_lo = xs[o + 512 * LO], x_hi = xs[o + 512 * HI];
+    const double x_lo = xs[o + TB * LO], x_hi = xs[o + TB * HI];
     const double a_lo = x_lo * wr, a_hi = x_hi * wr;
     xz_lo += x_lo * wzr;
     xz_hi += x_hi * wzr;
 #pragma unroll
     for (int k = 0; k <= PT; ++k) {
-      const double b = xs[o + 512 * (k <= LO ? k : k - LO - 1)];
+      const double b = xs[o + TB * (k <= LO ? k : k - LO - 1)];
       acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
     }
   }
 }
 
-template <bool DIAG>
-__device__ __forceinline__ void wait_blk(bool next_in_flight) {
-  if (next_in_flight) {
-    wait_vm<(DIAG ? 4 : 8) + 1>();
-  } else {
-    wait_vm<0>();
-  }
-}
-
+// Pipeline per piece (two LDS buffers, one barrier per block):
+//   wait for this wave's DMA of block blk; barrier (every wave's DMA of blk has landed and
+//   every wave is done reading the other buffer); DMA block blk+1 into the other buffer;
+//   MFMAs of block blk.  The DMA of blk+1 flies under blk's MFMAs, and the second
+//   workgroup on the CU covers whatever latency is left.
 template <int Q>
-__device__ void diag_item(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int wv, int lane,
-                          double* out) {
+__device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int wv, int lane,
+                           double* out) {
   d4 acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0;
-  const int s0 = (wv >> 2) * (RB / 8);
   wstage<true>(lds, 0, a, b0, I, I, wv, lane);
-  if (b0 + 1 < b1) wstage<true>(lds, 1, a, b0 + 1, I, I, wv, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
-    wait_blk<true>(blk + 1 < b1);
+    wait_vm<0>();
     lds_bar();
-    diag_block<Q>(lds, cur, lane, s0, acc, xz_lo, xz_hi);
-    lds_bar();
-    if (blk + 2 < b1) wstage<true>(lds, cur, a, blk + 2, I, I, wv, lane);
+    if (blk + 1 < b1) wstage<true>(lds, cur ^ 1, a, blk + 1, I, I, wv, lane);
+    diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
   }
-  // combine the two k-halves (wave q+4 -> LDS -> wave q), fixed order
   constexpr int LO = Q, HI = PT - 1 - Q;
+#pragma unroll
+  for (int k = 0; k <= PT; ++k) {
+    const int bi = k <= LO ? LO : HI, bj = k <= LO ? k : k - LO - 1;
+    const int t = bi * PT + bj;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j];
+  }
   xz_lo += __shfl_xor(xz_lo, 16);
   xz_lo += __shfl_xor(xz_lo, 32);
   xz_hi += __shfl_xor(xz_hi, 16);
   xz_hi += __shfl_xor(xz_hi, 32);
-  double* scr = lds + OFF_X + Q * (9 * 256 + 32);
-  if (wv >= 4) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) scr[k * 256 + 64 * j + lane] = acc[k][j];
-    if (lane < 16) {
-      scr[9 * 256 + lane] = xz_lo;
-      scr[9 * 256 + 16 + lane] = xz_hi;
-    }
-  }
-  lds_bar();
-  if (wv < 4) {
-#pragma unroll
-    for (int k = 0; k <= PT; ++k) {
-      const int bi = k <= LO ? LO : HI, bj = k <= LO ? k : k - LO - 1;
-      const int t = bi * PT + bj;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j] + scr[k * 256 + 64 * j + lane];
-    }
-    if (lane < 16) {
-      out[PT * PT * 256 + 16 * LO + lane] = xz_lo + scr[9 * 256 + lane];
-      out[PT * PT * 256 + 16 * HI + lane] = xz_hi + scr[9 * 256 + 16 + lane];
-    }
+  if (lane < 16) {
+    out[PT * PT * 256 + 16 * LO + lane] = xz_lo;
+    out[PT * PT * 256 + 16 * HI + lane] = xz_hi;
   }
 }
 
-__device__ void offdiag_item(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int wv,
-                             int lane, double* out) {
-  d4 acc[8];
+__device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int wv,
+                              int lane, double* out) {
+  d4 acc[16];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < 16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  const int dbg = a.dbg;
   wstage<false>(lds, 0, a, b0, I, J, wv, lane);
-  if (b0 + 1 < b1) wstage<false>(lds, 1, a, b0 + 1, I, J, wv, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
-    wait_blk<false>(blk + 1 < b1);
-    lds_bar();
+    wait_vm<0>();
+    if (!(dbg & 32)) lds_bar();
+    if (blk + 1 < b1 && (!(dbg & 4) || blk == b0)) wstage<false>(lds, cur ^ 1, a, blk + 1, I, J, wv, lane);
     offdiag_block(lds, cur, wv, lane, acc);
-    lds_bar();
-    if (blk + 2 < b1) wstage<false>(lds, cur, a, blk + 2, I, J, wv, lane);
   }
-  const int tr0 = 2 * (wv >> 1), tc0 = 4 * (wv & 1);
+  const int tr0 = 4 * (wv >> 1), tc0 = 4 * (wv & 1);
 #pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2)
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = (tr0 + t2) * PT + tc0 + u;
+      const int ti = (tr0 + t) * PT + tc0 + u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t2 * 4 + u][j];
+      for (int j = 0; j < 4; ++j) out[ti * 256 + 64 * j + lane] = acc[4 * t + u][j];
     }
 }
 
 }  // namespace
 
-// Work item it = (super-tile st, row split s), st = I(I+1)/2 + J.  Workgroup b runs on XCD
-// b % 8; items are dealt to XCDs in contiguous ranges so that the concurrently running
-// super-tiles of one row split share that XCD's L2.
-__global__ void __launch_bounds__(64 * NWAVE, 1) wide_gram_kernel(WideGramArgs a) {
+// Persistent Gram kernels (one for the off-diagonal, one for the diagonal super-tiles, so
+// each gets the whole register file): workgroup g runs the pieces [wg_begin[g],
+// wg_begin[g+1]) of the cost-balanced schedule built on the host (engine.cpp).
+template <bool DIAG>
+__global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a) {
   __shared__ double lds[LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int it = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
-  if (it >= a.nitems) return;
-  const int s = it / a.nst, st = it - s * a.nst;
-  int I = 0;
-  while ((I + 1) * (I + 2) / 2 <= st) ++I;
-  const int J = st - I * (I + 1) / 2;
-  const int64_t b0 = (a.nblocks * s) / a.nsplit, b1 = (a.nblocks * (s + 1)) / a.nsplit;
-  double* out = a.partials + ((int64_t)st * a.nsplit + s) * a.stride;
-  if (b0 >= b1) {  // empty row range: zero partial
-    for (int e = threadIdx.x; e < a.stride; e += 64 * NWAVE) out[e] = 0.0;
-    return;
-  }
-  if (I != J) {
-    offdiag_item(lds, a, I, J, b0, b1, wv, lane, out);
-  } else {
-    switch (wv & 3) {
-      case 0: diag_item<0>(lds, a, I, b0, b1, wv, lane, out); break;
-      case 1: diag_item<1>(lds, a, I, b0, b1, wv, lane, out); break;
-      case 2: diag_item<2>(lds, a, I, b0, b1, wv, lane, out); break;
-      default: diag_item<3>(lds, a, I, b0, b1, wv, lane, out); break;
+  const int pb = a.wg_begin[blockIdx.x], pe = a.wg_begin[blockIdx.x + 1];
+#pragma unroll 1
+  for (int pc = pb; pc < pe; ++pc) {
+    const WidePiece pz = a.pieces[pc];
+    const int st = pz.st;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= st) ++I;
+    const int J = st - I * (I + 1) / 2;
+    double* out = a.partials + (int64_t)pz.slot * a.stride;
+    if constexpr (!DIAG) {
+      offdiag_piece(lds, a, I, J, pz.b0, pz.b1, wv, lane, out);
+    } else {
+      switch (wv) {
+        case 0: diag_piece<0>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 1: diag_piece<1>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 2: diag_piece<2>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        default: diag_piece<3>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+      }
     }
+    lds_bar();  // every wave is done with both buffers before the next piece stages
   }
 }
 
@@ -305,8 +292,8 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
 }
 
 // Packed output: lower-tri X'WX row-major | X'Wz | NS scalars, summed in a fixed order.
-__global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stride, int nsplit, int p,
-                                   const double* __restrict__ rowpart, int nrow, double* __restrict__ out) {
+__global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stride, const int* __restrict__ st_range,
+                                   int p, const double* __restrict__ rowpart, int nrow, double* __restrict__ out) {
   const int64_t tri = (int64_t)p * (p + 1) / 2;
   const int64_t total = tri + p + NS;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -326,8 +313,9 @@ __global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stri
         st = I * (I + 1) / 2 + I;
         src = PT * PT * 256 + (c % PANEL);
       }
-      const double* ps = part + st * nsplit * stride + src;
-      for (int g = 0; g < nsplit; ++g) s += ps[(int64_t)g * stride];
+      const int g0 = st_range[2 * st], g1 = st_range[2 * st + 1];
+      const double* ps = part + src;
+      for (int g = g0; g < g1; ++g) s += ps[(int64_t)g * stride];
     } else {
       const int k = (int)(e - tri - p);
       for (int g = 0; g < nrow; ++g) s += rowpart[(int64_t)g * NS + k];
@@ -380,17 +368,22 @@ hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_wide_gram(const WideGramArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(wide_gram_kernel, dim3(8 * a.per_xcd), dim3(64 * NWAVE), 0, st, a);
+int wide_gram_wg_per_cu() { return 2; }
+
+hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st) {
+  if (diag)
+    hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(64 * NWAVE), 0, st, a);
+  else
+    hipLaunchKernelGGL(wide_gram_kernel<false>, dim3(grid), dim3(64 * NWAVE), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_wide_reduce(const double* part, int64_t stride, int nsplit, int p, const double* rowpart, int nrow,
-                              double* out, hipStream_t st) {
+hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,
+                              int nrow, double* out, hipStream_t st) {
   const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(wide_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, stride, nsplit, p, rowpart, nrow, out);
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, stride, st_range, p, rowpart, nrow, out);
   return hipGetLastError();
 }
 

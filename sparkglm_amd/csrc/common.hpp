@@ -84,7 +84,7 @@ constexpr int WIDE_RB = 16;   // rows per Gram-kernel LDS block
 struct WideGramArgs {
   const double* X;
   int64_t ld;
-  int ncols;            // columns stored (multiple of 4, zero past p)
+  int ncols;            // columns stored (multiple of 8, zero past p)
   const double* w;
   const double* wz;
   const WidePiece* pieces;

@@ -325,7 +325,7 @@ struct sglm_engine : public Backend {
     nblocks = (n + RB - 1) / RB;
     n_pad = std::max<int64_t>(nblocks, 1) * RB;
     const size_t vb = sizeof(double) * (size_t)n_pad;
-    const size_t ncols = (size_t)((p + 3) / 4 * 4);  // whole column quads for the LDS-DMA staging
+    const size_t ncols = (size_t)((p + 7) / 8 * 8);  // whole column octets for the LDS-DMA staging
     hipError_t e = hipMalloc(&dX, vb * ncols);
     if (e != hipSuccess) {
       set_error(hip_msg(e, "hipMalloc(X)"));
@@ -422,7 +422,7 @@ struct sglm_engine : public Backend {
       WideGramArgs g{};
       g.X = dX;
       g.ld = n_pad;
-      g.ncols = (int)((p + 3) / 4 * 4);
+      g.ncols = (int)((p + 7) / 8 * 8);
       g.w = dw;
       g.wz = dwz;
       g.partials = dgp;

@@ -60,52 +60,71 @@ constexpr int NWAVE = 4;                   // one wave per SIMD; two workgroups 
 __device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
 
 // Stage block blk of panels I (and J unless DIAG) into buffer buf: one global_load_lds of
-// 16 bytes per lane moves an "octet" of 8 columns x 16 rows; 16 octets per panel.
+// 16 bytes per lane moves an "octet" of 8 columns x 16 rows; 16 octets per panel.  The
+// source address is a wave-uniform part (octet column, block row: SGPRs) plus one of two
+// per-lane offsets (column within the octet, swizzled row pair; swz depends only on the
+// octet's parity), so no per-octet addresses stay live in VGPRs.  Octets past the stored
+// columns (a multiple of 8) are skipped: they only feed tiles beyond p.
 template <bool DIAG>
 __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs& a, int64_t blk, int I, int J, int wv,
-                                       int lane) {
+                                       const int64_t (&loff)[2], int lane) {
   constexpr int OW = DIAG ? 4 : 8;  // octets per wave
-  const int64_t r0 = blk * WRB;
-  const int i = lane & 7, oc = lane >> 3;
+  const double* xb = a.X + blk * WRB;
 #pragma unroll
   for (int k = 0; k < OW; ++k) {
     const int qq = wv * OW + k;  // 0..15 panel I, 16..31 panel J
     const int ps = qq >> 4, ol = qq & 15;
-    const int cp = ol * 8 + oc;                    // column within the panel
-    int gc = (ps ? J : I) * PANEL + cp;            // column of X
-    gc = gc < a.ncols ? gc : a.ncols - 1;          // columns past the stored ones: duplicates
-    const double* src = a.X + (int64_t)gc * a.ld + r0 + ((2 * i) ^ swz(cp));
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16,
-                                     0, 0);
+    const int c0 = (ps ? J : I) * PANEL + ol * 8;  // first column of the octet (uniform)
+    if (c0 < a.ncols)
+      __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
+                                       (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16, 0, 0);
   }
   const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
-  const double* vsrc = (v ? a.wz : a.w) + r0 + 2 * lane;
+  const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
   if (lane < WRB / 2)
     __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
 }
 
+// Per-lane DMA offsets (doubles) for even / odd octets: column oc = lane >> 3 of the octet,
+// rows (2i, 2i+1) ^ swz(column), i = lane & 7.
+__device__ __forceinline__ void lane_offsets(const WideGramArgs& a, int lane, int64_t (&loff)[2]) {
+  const int i = lane & 7, oc = lane >> 3;
+#pragma unroll
+  for (int par = 0; par < 2; ++par) loff[par] = (int64_t)oc * a.ld + ((2 * i) ^ swz(8 * par + oc));
+}
+
 // Off-diagonal super-tile: wave wv owns tile rows 4(wv>>1)+{0..3} of panel I and tile
-// columns 4(wv&1)+{0..3} of panel J (16 tiles).  A = X_I * w (row-scaled), B = X_J.
+// columns 4(wv&1)+{0..3} of panel J (16 tiles).  A = X_I * w (row-scaled), B = X_J.  The
+// operands of k-step s+1 are read from LDS while the 16 MFMAs of step s issue.
 __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[16]) {
   const int cl = lane & 15, rq = lane >> 4;
   const int f = 2 * (cl >> 1);
   const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB + TB * (4 * (wv >> 1));
   const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * WRB + TB * (4 * (wv & 1));
   const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
-#pragma unroll 2
-  for (int s = 0; s < WRB / 4; ++s) {
+  double av[2][4], bv[2][4], wr[2];
+  auto load = [&](int s, int slot) {
     const int r = 4 * s + rq;
     const int o = r ^ f;
-    const double wr = w[r];
-    double av[4], bv[4];
+    wr[slot] = w[r];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) av[t] = xI[o + TB * t] * wr;
+    for (int t = 0; t < 4; ++t) av[slot][t] = xI[o + TB * t];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) bv[u] = xJ[o + TB * u];
+    for (int u = 0; u < 4; ++u) bv[slot][u] = xJ[o + TB * u];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int s = 0; s < WRB / 4; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < WRB / 4) load(s + 1, cur ^ 1);
+    double as[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) as[t] = av[cur][t] * wr[cur];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[4 * t + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[u], acc[4 * t + u], 0, 0, 0);
+      for (int u = 0; u < 4; ++u)
+        acc[4 * t + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[t], bv[cur][u], acc[4 * t + u], 0, 0, 0);
   }
 }
 
@@ -149,13 +168,15 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0;
-  wstage<true>(lds, 0, a, b0, I, I, wv, lane);
+  int64_t loff[2];
+  lane_offsets(a, lane, loff);
+  wstage<true>(lds, 0, a, b0, I, I, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
     wait_vm<0>();
     lds_bar();
-    if (blk + 1 < b1) wstage<true>(lds, cur ^ 1, a, blk + 1, I, I, wv, lane);
+    if (blk + 1 < b1) wstage<true>(lds, cur ^ 1, a, blk + 1, I, I, wv, loff, lane);
     diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
   }
   constexpr int LO = Q, HI = PT - 1 - Q;
@@ -182,13 +203,15 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   const int dbg = a.dbg;
-  wstage<false>(lds, 0, a, b0, I, J, wv, lane);
+  int64_t loff[2];
+  lane_offsets(a, lane, loff);
+  wstage<false>(lds, 0, a, b0, I, J, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
     wait_vm<0>();
     if (!(dbg & 32)) lds_bar();
-    if (blk + 1 < b1 && (!(dbg & 4) || blk == b0)) wstage<false>(lds, cur ^ 1, a, blk + 1, I, J, wv, lane);
+    if (blk + 1 < b1 && (!(dbg & 4) || blk == b0)) wstage<false>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
     offdiag_block(lds, cur, wv, lane, acc);
   }
   const int tr0 = 4 * (wv >> 1), tc0 = 4 * (wv & 1);

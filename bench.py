@@ -7,7 +7,8 @@ seeded synthetic generator (sparkglm_amd.synth; bit-identical host copy).  A "st
 one IRLS iteration: the fused pass over every resident row (eta, mu, w, z, deviance and
 the X'WX / X'Wz Gramian on fp64 MFMA) + the all-reduce over ranks + the p x p solve.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--p P]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload logit256|poisson64|gamma2048|logit512]
+                  [--rows R] [--p P]
 
 N > 1 is launched by torch.distributed.run (one process per GPU); each rank holds its
 own 100M-row shard (weak scaling) and the per-iteration Gram all-reduce runs on RCCL
@@ -35,31 +36,55 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(p: int, seed: int, rows: int, threads: int) -> dict:
+# BASELINE.json configs -> bench workloads.  The default (N=1 headline) is configs[1]; the others
+# are measured with --workload and recorded under profiles/ (rows per GPU = the config's global
+# rows / 8 where the config is quoted on 8 GPUs, or the largest resident shard, as labelled).
+WORKLOADS = {
+    "logit256": dict(cfg=1, kind=0, family="binomial", link="logit", p=256, rows=100_000_000, seed=2,
+                     cpu_rows=2_000_000,
+                     label="binomial/logit glm, dense fp64 design, IRLS (BASELINE configs[1])"),
+    "poisson64": dict(cfg=2, kind=2, family="poisson", link="log", p=64, rows=125_000_000, seed=3,
+                      cpu_rows=8_000_000,
+                      label="poisson/log glm with offset + prior weights, 1B x 64 row-sharded over 8 GPUs "
+                            "= 125M rows per GPU (BASELINE configs[2])"),
+    "gamma2048": dict(cfg=3, kind=3, family="gamma", link="inverse", p=2048, rows=12_500_000, seed=4,
+                      cpu_rows=40_000,
+                      label="gamma/inverse glm, 50M x 2048 wide design over 4 GPUs = 12.5M rows per GPU, "
+                            "GPU Cholesky (BASELINE configs[3])"),
+    "logit512": dict(cfg=4, kind=0, family="binomial", link="logit", p=512, rows=60_000_000, seed=5,
+                     cpu_rows=300_000,
+                     label="binomial/logit glm, p = 512 (BASELINE configs[4]); 2B x 512 = 8.19 TB is not "
+                           "HBM-resident on 8 GPUs, so each GPU holds the largest resident shard, 60M rows"),
+}
+
+
+def cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
     """The CPU restatement (oracle/, test infrastructure) timed on a bounded sample."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import pyoracle  # noqa: E402  (checker / CPU baseline only)
     from sparkglm_amd import synth
 
-    X, y, _, _ = synth.generate(0, 0, rows, p, seed)
+    X, y, off, prior = synth.generate(wl["kind"], 0, rows, p, wl["seed"])
     t0 = time.perf_counter()
-    fit = pyoracle.fit_glm(X, y, "binomial", "logit", npart=threads, nthreads=threads)
+    fit = pyoracle.fit_glm(X, y, wl["family"], wl["link"], offset=off, prior=prior, npart=threads,
+                           nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": rows * fit.iter / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"CPU restatement of fitMultipleBinomial (oracle/sglm_oracle.c, -O3 AVX2, OpenMP), "
-                      f"{rows} x {p} logit rows of the same generator, {threads} partitions/threads, "
-                      f"{fit.iter} IRLS iterations to convergence in {dt:.2f} s (not the JVM)",
+            "sample": f"CPU restatement of fitMultipleBinomial's IRLS (oracle/sglm_oracle.c, -O3 AVX2, OpenMP), "
+                      f"{rows} x {p} {wl['family']}/{wl['link']} rows of the same generator, {threads} "
+                      f"partitions/threads, {fit.iter} IRLS iterations to convergence in {dt:.2f} s (not the JVM)",
             "time_to_converge_s": dt, "iters": fit.iter}
 
 
-def pmc_traffic(p: int, n: int):
-    """Per-launch HBM bytes of the fused pass: the per-row FETCH_SIZE + WRITE_SIZE measured by
-    rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
+def pmc_traffic(p: int, n: int, family: str):
+    """Per-launch HBM bytes of the dominant kernel: the per-row FETCH_SIZE + WRITE_SIZE measured
+    by rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
     times the rows of this launch (the pass streams every row exactly once)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            e = json.load(f).get(str(p))
+            tab = json.load(f)
+        e = tab.get(f"{family}:{p}", tab.get(str(p)) if family == "binomial" else None)
         return None if e is None else e["bytes_per_row"] * n
     except (OSError, ValueError, KeyError):
         return None
@@ -70,13 +95,15 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
-    ap.add_argument("--p", type=int, default=256)
-    ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--cpu-rows", type=int, default=2_000_000)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="logit256")
+    ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default: the workload's)")
+    ap.add_argument("--p", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--cpu-rows", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -98,10 +125,13 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
-    n, p = args.rows, args.p
+    n = args.rows or wl["rows"]
+    p = args.p or wl["p"]
+    seed = wl["seed"] if args.seed is None else args.seed
+    fam, lnk = wl["family"], wl["link"]
     eng = Engine(local)
     t0 = time.perf_counter()
-    eng.synth(0, rank * n, n, p, args.seed)  # this rank's shard of the global design
+    eng.synth(wl["kind"], rank * n, n, p, seed)  # this rank's shard of the global design
     gen_s = time.perf_counter() - t0
     if dist_on:
         if args.comm == "rccl":
@@ -111,23 +141,24 @@ def main() -> int:
         else:
             from sparkglm_amd.distributed import torch_allreduce
             eng.set_comm(torch_allreduce(), on_device=True)
-    log(f"[rank {rank}] shard {n} x {p} generated in {gen_s:.2f} s")
+    log(f"[rank {rank}] shard {n} x {p} ({args.workload}) generated in {gen_s:.2f} s")
 
     # time-to-converge: a full fit (data resident), reference semantics (tol 1e-6)
     barrier()
     t0 = time.perf_counter()
-    fit = eng.fit_glm("binomial", "logit", tol=1e-6)
+    fit = eng.fit_glm(fam, lnk, tol=1e-6)
     barrier()
     ttc = time.perf_counter() - t0
     log(f"[rank {rank}] converged in {fit.iter} iterations, {ttc:.3f} s, deviance {fit.deviance!r}")
 
-    beta = np.zeros(p)
+    # timed IRLS iterations from the fitted coefficients (a valid eta for every family)
+    beta = np.array(fit.coefs, dtype=np.float64)
     if args.warmup > 0:
-        beta, _ = eng.irls_iterations(beta, args.warmup)
+        beta, _ = eng.irls_iterations(beta, args.warmup, fam, lnk)
     eng.reset_stats()
     barrier()
     t0 = time.perf_counter()
-    beta, dev = eng.irls_iterations(beta, args.steps)
+    beta, dev = eng.irls_iterations(beta, args.steps, fam, lnk)
     barrier()
     dt = time.perf_counter() - t0
     st = eng.stats()
@@ -138,10 +169,32 @@ def main() -> int:
 
     if rank == 0:
         total_rows = n * world
-        kern_ms = st["pass_kernel_ms"] / max(st["passes"], 1)
-        flops = n * (p * (p + 1) + 2 * p)  # SYRK-convention X'WX + X'Wz per launch
-        achieved = flops / (kern_ms * 1e-3) / 1e12
-        traffic = pmc_traffic(p, n)
+        passes = max(st["passes"], 1)
+        wide = st["path"] == 1
+        nvec = 1 + (2 if wl["kind"] == 2 else 0)  # y (+ offset, prior)
+        flops = n * (p * (p + 1) + 2 * p)      # SYRK-convention X'WX + X'Wz per launch
+        bytes_pass = n * (8 * p + 8 * nvec)    # X row + per-row vectors, read once per pass
+        if wide:
+            kern = "wide_gram_kernel"
+            kern_ms = st["gram_kernel_ms"] / passes
+            pass_ms = (st["gram_kernel_ms"] + st["row_kernel_ms"]) / passes
+        else:
+            kern = f"irls_pass_kernel<{(p + 15) // 16 + ((p + 15) // 16) % 2},{fam},{lnk}>"
+            kern_ms = st["pass_kernel_ms"] / passes
+            pass_ms = kern_ms
+        tflops = flops / (kern_ms * 1e-3) / 1e12
+        gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(p, n, fam)
+        if wl["cfg"] == 2:  # HBM-bound fused pass (AI ~ 8 flop/B <= ridge)
+            roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": kern_ms,
+                    "algorithmic_bytes_per_launch": bytes_pass,
+                    "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS}
+        else:
+            roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                    "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
+                    "hbm_gbs_algorithmic": gbs}
         out = {
             "metric": METRIC,
             "value": total_rows * args.steps / dt,
@@ -155,25 +208,23 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded counter-based generator, generated in HBM)",
-            "config": {"workload": "binomial/logit glm, dense fp64 design, IRLS (BASELINE configs[1])",
+            "config": {"workload": wl["label"], "bench_workload": args.workload,
                        "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}",
-                       "family": "binomial", "link": "logit", "tol": 1e-6},
+                       "family": fam, "link": lnk, "tol": 1e-6,
+                       "offset_prior": wl["kind"] == 2},
             "time_to_converge_s": ttc,
             "iters_to_converge": fit.iter,
             "deviance": fit.deviance,
-            "roofline": {"bound": "mfma", "kernel": "irls_pass_kernel<16,binomial,logit>",
-                         "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
-                         "hbm_gbs_algorithmic": n * 8 * (p + 1) / (kern_ms * 1e-3) / 1e9},
-            "breakdown_ms_per_step": {"fused_pass": kern_ms,
-                                      "reduce": st["reduce_kernel_ms"] / max(st["passes"], 1),
+            "roofline": roof,
+            "breakdown_ms_per_step": {"pass_kernels": pass_ms,
+                                      "row_kernel": st["row_kernel_ms"] / passes if wide else None,
+                                      "reduce": st["reduce_kernel_ms"] / passes,
                                       "solve": st["solve_ms"] / args.steps,
                                       "comm": st["comm_ms"] / args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(p, args.seed, args.cpu_rows, threads)
+            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

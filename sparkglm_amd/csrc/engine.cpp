@@ -83,6 +83,8 @@ struct sglm_engine : public Backend {
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
+  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; SGLM_NARROW=0 disables
+  bool narrow = false, allow_narrow = true;
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
   int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
@@ -278,11 +280,21 @@ struct sglm_engine : public Backend {
       int rc = ensure_wide_workspace();
       if (rc) return rc;
     }
-    if (!wide) P16 = pass_variant((int)p);
-    stride = wide ? 0 : pass_stride(P16);
-    if (!wide) {
-      const int64_t want_grid = (int64_t)ncu * pass_wg_per_cu(P16);
-      grid = (int)(nblocks < want_grid ? (nblocks > 0 ? nblocks : 1) : want_grid);
+    narrow = !wide && allow_narrow && p <= 64;
+    if (narrow) {
+      P16 = narrow_variant((int)p);
+      stride = narrow_stride(P16);
+      const int64_t want_grid = (int64_t)ncu * narrow_wg_per_cu();
+      const int64_t per_wg = narrow_rows_per_wg();
+      const int64_t need = (nblocks * RB + per_wg - 1) / per_wg;
+      grid = (int)std::max<int64_t>(1, std::min(need, want_grid));
+    } else {
+      if (!wide) P16 = pass_variant((int)p);
+      stride = wide ? 0 : pass_stride(P16);
+      if (!wide) {
+        const int64_t want_grid = (int64_t)ncu * pass_wg_per_cu(P16);
+        grid = (int)(nblocks < want_grid ? (nblocks > 0 ? nblocks : 1) : want_grid);
+      }
     }
     const int64_t need_part = std::max<int64_t>((int64_t)grid * stride, 4096 * NS);
     if (need_part > part_cap) {
@@ -438,7 +450,8 @@ struct sglm_engine : public Backend {
       HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dred, st));
     } else {
       if (nblocks > 0) {
-        HIPCHK(launch_pass(P16, a, grid, st));
+        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st));
+        else HIPCHK(launch_pass(P16, a, grid, st));
       } else {
         HIPCHK(hipMemsetAsync(dpart, 0, sizeof(double) * stride, st));
       }
@@ -747,6 +760,7 @@ int sglm_create(int device, sglm_engine** out) {
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char* ab = std::getenv("SGLM_DEBUG_ABLATE")) h->dbg = std::atoi(ab);
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
+  if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   *out = h;
   return SGLM_OK;
 }
@@ -784,8 +798,8 @@ int sglm_set_data_device(sglm_engine* h, const double* dX, int64_t n, int64_t p,
 
 int sglm_synth(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed) {
   if (int rc = check_handle(h)) return rc;
-  if (kind < 0 || kind > 2 || n <= 0 || p <= 0 || row0 < 0) {
-    set_error("requirement failed: synth kind in {0,1,2}, n >= 1, p >= 1");
+  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
+    set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
     return SGLM_EINVAL;
   }
   int rc = h->alloc_data(n, p, false, kind == 2, kind == 2);
@@ -953,7 +967,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->p = h->p;
   out->workgroups = h->grid;
   out->kernel_variant = h->P16;
-  out->path = h->wide ? 1 : 0;
+  out->path = h->wide ? 1 : (h->narrow ? 2 : 0);
   out->wide_panels = h->wide ? h->npan : 0;
   out->row_kernel_ms = h->row_ms;
   out->gram_kernel_ms = h->wide ? h->gram_ms : h->pass_ms;

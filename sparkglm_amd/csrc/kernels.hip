@@ -198,18 +198,22 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
 // tile grid: tiles (LO, 0..LO) then (HI, 0..HI).  Lane l reads X[k0 + (l>>4)][16b + (l&15)];
 // the A operand (blocks LO / HI) is scaled by the lane's row weight, the B operands are
 // used straight from LDS.  X'Wz accumulates on the VALU from the same A fragments.
+// A phase is RB/8 k-steps starting at S0.  Narrow variants (P16 <= 8: at most 9 MFMAs per
+// k-step) unroll the phase so the next k-step's LDS operand reads issue under the current
+// k-step's MFMAs; wide variants carry enough MFMAs per k-step to cover the read latency.
 template <int P16, int WV>
-__device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0, int S1,
+__device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0,
                                            d4 (&acc)[P16 + 1], double& xz_lo, double& xz_hi) {
   using G = Geo<P16>;
   constexpr int LO = WV, HI = P16 - 1 - WV;
+  constexpr int UNR = P16 <= 8 ? RB / 8 : 1;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* w = lds + G::OFF_W + wb * 2 * RB;
   const int cl = lane & 15, rq = lane >> 4;
   const double* colbase = xs + cl * 32;  // column c = 16b + cl has (2c & 31) == 2cl for every b
-#pragma unroll 1
-  for (int s = S0; s < S1; ++s) {
-    const int r = 4 * s + rq;
+#pragma unroll UNR
+  for (int j = 0; j < RB / 8; ++j) {
+    const int r = 4 * (S0 + j) + rq;
     const double* base = colbase + (r ^ (2 * cl));
     const double wr = w[r], wzr = w[RB + r];
     const double x_lo = base[512 * LO], x_hi = base[512 * HI];
@@ -223,22 +227,6 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
       const double b = base[512 * (k <= LO ? k : k - LO - 1)];
       acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
     }
-  }
-}
-
-template <int P16>
-__device__ __forceinline__ void gram_dispatch(int wv, const double* lds, int buf, int wb, int lane, int S0, int S1,
-                                              d4 (&acc)[P16 + 1], double& xz_lo, double& xz_hi) {
-  static_assert(P16 <= 16, "variant");
-  switch (wv) {
-    case 0: gram_steps<P16, 0>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 1: if constexpr (P16 >= 4) gram_steps<P16, 1>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 2: if constexpr (P16 >= 6) gram_steps<P16, 2>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 3: if constexpr (P16 >= 8) gram_steps<P16, 3>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 4: if constexpr (P16 >= 10) gram_steps<P16, 4>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 5: if constexpr (P16 >= 12) gram_steps<P16, 5>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    case 6: if constexpr (P16 >= 14) gram_steps<P16, 6>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
-    default: if constexpr (P16 >= 16) gram_steps<P16, 7>(lds, buf, wb, lane, S0, S1, acc, xz_lo, xz_hi); break;
   }
 }
 
@@ -285,8 +273,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
       }
       const bool rows = has_next && ((ph == 1 && early_rows) || (ph == 2 && !early_rows));
       const bool mfma = has_gram && (ph == 0 || (ph == 1 && !early_rows) || (ph == 2 && early_rows));
-      if (mfma) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, ph == 0 ? 0 : RB / 8, ph == 0 ? RB / 8 : RB / 4, acc,
-                                    xz_lo, xz_hi);
+      if (mfma) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, ph == 0 ? 0 : RB / 8, acc, xz_lo, xz_hi);
       if (rows && !(a.dbg & 1)) {
         __builtin_amdgcn_s_setprio(1);  // the row stage is on the critical path; the partner wave's MFMAs are not
         row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
@@ -471,11 +458,15 @@ __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t 
       double x;
       if (j == 0) {
         x = 1.0;
+      } else if (kind == 3) {  // positive design: eta > 0 for the inverse link
+        x = (0.5 + unif(kx + gi * (uint64_t)p + (uint64_t)j)) * scale;
       } else {
         x = (2.0 * unif(kx + gi * (uint64_t)p + (uint64_t)j) - 1.0) * scale;
       }
       X[(int64_t)j * ld + i] = x;
-      const double bj = (j == 0) ? -0.25 : 0.5 * (double)((j % 5) - 2);
+      double bj;
+      if (kind == 3) bj = (j == 0) ? 1.0 : 0.1 * (double)((j % 5) + 1);
+      else bj = (j == 0) ? -0.25 : 0.5 * (double)((j % 5) - 2);
       const double prod = x * bj;
       eta = eta + prod;
     }
@@ -486,6 +477,8 @@ __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t 
       y[i] = u < pr ? 1.0 : 0.0;
     } else if (kind == 1) {
       y[i] = eta + (2.0 * u - 1.0);
+    } else if (kind == 3) {
+      y[i] = (0.25 + 1.5 * u) / eta;  // mean 1/eta (gamma / inverse link), y > 0
     } else {
       double lam = 1.0 + 0.5 * eta;
       lam = lam < 0.1 ? 0.1 : lam;

@@ -21,6 +21,13 @@ hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hip
 hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,
                         double* y, double* m, double* off, double* prior, hipStream_t st);
 
+// narrow path (narrow.hip): p <= 64
+int narrow_variant(int p);      // column blocks of 16 (1..4)
+int narrow_stride(int P16);     // doubles per workgroup partial (reduce_partials_kernel layout)
+int narrow_wg_per_cu();
+int narrow_rows_per_wg();       // rows one workgroup streams per block step (waves x 16)
+hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st);
+
 // wide path (wide.hip)
 int wide_panels(int p);
 int64_t wide_stride();

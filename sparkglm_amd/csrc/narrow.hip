@@ -1,0 +1,333 @@
+// narrow.hip -- the narrow-design (p <= 64) fused IRLS pass for gfx950.
+//
+// At p <= 64 one row of X is <= 536 bytes and the pass sits at the HBM / fp64-MFMA balance
+// point (~8 flop/B), so the workgroup-lockstep pipeline of irls_pass_kernel
+// (two barriers per row block, row stage on one wave while its partners wait) leaves both
+// the MFMA pipe and HBM idle.  Here every wave is an independent streaming pipeline with
+// no barriers in its main loop:
+//
+//   * wave gw owns a contiguous range of row blocks (NRB = 32 rows for p <= 32, 16 above)
+//     and the WHOLE lower-triangular Gram
+//     (T = P16(P16+1)/2 <= 10 16x16 fp64 tiles, <= 80 accumulator VGPRs);
+//   * its blocks land in a wave-private, double-buffered LDS image by LDS-DMA
+//     (global_load_lds_dwordx4; block i+2 is issued as soon as block i is consumed), one
+//     wave-instruction per column octet plus one for the y/m/offset/prior values;
+//   * row stage (etaCreate GLM.scala:321-332, zwCreateBinomial GLM.scala:359-395, deviance
+//     GLM.scala:162-170): 64/NRB lanes per row form eta over interleaved columns (xor-16 /
+//     xor-32 lane swaps), then the family arithmetic (rowmath.hpp) on NRB lanes, w and w*z
+//     to LDS;
+//   * Gramian on v_mfma_f64_16x16x4_f64, A operand scaled by w, X'Wz on the VALU
+//     (partitionComponents, utils.scala:84-92);
+//   * two waves per SIMD (8 per workgroup, one workgroup per CU) interleave MFMA and VALU
+//     work; the 8 wave partials are summed in LDS in a fixed tree order after the loop and
+//     one partial per workgroup goes to reduce_partials_kernel (deterministic).
+//
+// LDS image of one block (per wave, per buffer): column c at c*NRB doubles, row r in slot
+// r ^ f(c) (swz below), applied on the DMA source address.  MFMA fragment reads (lane
+// (rq, cl) reads row 4s+rq of column 16b+cl) and row-stage reads (lane (g, rl) reads row rl
+// of column (64/NRB)u+g) are both bank-conflict free for ds_read_b64.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "rowmath.hpp"
+
+namespace sglm {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int NWAVE = 8;   // waves per workgroup (two per SIMD), one workgroup per CU
+
+// Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
+// (LDS: 8 waves x 2 buffers).  Row swizzle f(c): 2((c >> 1) & 7) at NRB = 16 (the column
+// parity separates the bank halves), 2(c & 15) at NRB = 32.
+template <int P16>
+struct NGeo {
+  static_assert(P16 >= 1 && P16 <= 4, "narrow variants: p <= 64");
+  static constexpr int NRB = P16 <= 2 ? 32 : 16;     // rows per block
+  static constexpr int LPR = 64 / NRB;               // row-stage lanes per row
+  static constexpr int NC = 16 * P16;                // padded columns
+  static constexpr int T = P16 * (P16 + 1) / 2;      // lower-triangular tiles
+  static constexpr int CPI = 128 / NRB;              // columns per DMA wave-instruction (1 KiB)
+  static constexpr int NOCT = NC / CPI;              // DMA wave-instructions for X per block
+  static constexpr int SPER = NRB == 16 ? 2 : 16 / CPI;  // period of the swizzle over column groups
+  static constexpr int LPER = NOCT < SPER ? NOCT : SPER;
+  static constexpr int XB = NC * NRB;                // doubles of X per buffer
+  static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
+  static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB]
+  static constexpr int WAVE_LDS = OFF_W + 2 * NRB;   // doubles per wave
+  static constexpr int PSZ = T * 256 + NC + 2;       // one wave partial (tiles | X'Wz | dev, sum w)
+  static constexpr int LDS = (NWAVE * WAVE_LDS > 4 * PSZ) ? NWAVE * WAVE_LDS : 4 * PSZ;
+  static constexpr int STRIDE = T * 256 + NC + NS;   // global partial (reduce_partials_kernel layout)
+  static_assert(LDS * 8 <= 160 * 1024, "LDS budget");
+};
+
+template <int NRB>
+__device__ __forceinline__ constexpr int swz(int c) { return NRB == 16 ? 2 * ((c >> 1) & 7) : 2 * (c & 15); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ double xor16_sum(double v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
+// DMA of block blk into buffer buf of this wave's image: NOCT wave-instructions of CPI
+// columns x NRB rows (1 KiB each) + one for the block's slices of y, m, offset, prior
+// (4 x NRB doubles on 2 NRB lanes).  Column groups past the stored columns re-load the last
+// stored group (finite data; beta is 0 and the tiles are discarded past p), so every block
+// issues exactly NOCT + 1 vector-memory operations.
+template <int P16>
+__device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, int64_t blk, int ngrp_stored,
+                                       const int64_t (&loff)[NGeo<P16>::LPER], const double* vsrc, int lane) {
+  using G = NGeo<P16>;
+  const double* xb = a.X + blk * G::NRB;
+  double* dst = wl + buf * G::BUF;
+#pragma unroll
+  for (int o = 0; o < G::NOCT; ++o) {
+    const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
+    __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER]),
+                                     (lds_void*)(dst + o * 128), 16, 0, 0);
+  }
+  if (G::NRB == 32 || lane < 2 * G::NRB)
+    __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
+}
+
+template <int P16, int FAM, int LNK>
+__global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) {
+  using G = NGeo<P16>;
+  constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
+  __shared__ double lds[G::LDS];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* wl = lds + wv * G::WAVE_LDS;
+
+  const int64_t nb = a.nblocks * (RB / NRB);  // NRB-row blocks (n_pad = nblocks * RB)
+  const int64_t gw = (int64_t)blockIdx.x * NWAVE + wv, nwt = (int64_t)gridDim.x * NWAVE;
+  const int64_t b0 = nb * gw / nwt, b1 = nb * (gw + 1) / nwt;
+  const int ngrp_stored = ((a.p + 7) / 8 * 8) / G::CPI;  // X stores whole column octets
+  const bool irls = a.mode == MODE_IRLS;
+  const bool has_eta = irls && a.eta_out != nullptr;
+
+  // per-lane parts of the DMA source addresses: lane -> (column cc of the group, row pair j);
+  // the swizzle repeats every LPER column groups
+  int64_t loff[G::LPER];
+  {
+    const int cc = lane / (NRB / 2), j = lane % (NRB / 2);
+#pragma unroll
+    for (int o = 0; o < G::LPER; ++o) loff[o] = (int64_t)cc * a.ld + ((2 * j) ^ swz<NRB>(G::CPI * o + cc));
+  }
+  const double* vsrc;
+  {
+    const int v = (lane / (NRB / 2)) & 3;  // 0 y, 1 m, 2 offset, 3 prior (absent: y again)
+    const double* p = a.y;
+    if (v == 1 && a.m) p = a.m;
+    if (v == 2 && a.off) p = a.off;
+    if (v == 3 && a.prior) p = a.prior;
+    vsrc = p + 2 * (lane % (NRB / 2));
+  }
+  // row stage: lane (g, rl), g < LPR, covers columns LPR*u + g of row rl
+  const int g = lane / NRB, rl = lane % NRB;
+  double bcol[CPL];
+#pragma unroll
+  for (int u = 0; u < CPL; ++u) {
+    const int c = LPR * u + g;
+    bcol[u] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
+  }
+
+  d4 acc[G::T];
+#pragma unroll
+  for (int t = 0; t < G::T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  double xz[P16];
+#pragma unroll
+  for (int b = 0; b < P16; ++b) xz[b] = 0.0;
+  double s_dev = 0.0, s_aux = 0.0;
+
+  const int cl = lane & 15, rq = lane >> 4;
+  const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
+  const bool do_rows = !(a.dbg & 1), do_gram = !(a.dbg & 2), do_dma = !(a.dbg & 4);
+
+  if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
+  if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
+
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; ++blk) {
+    const int buf = (int)((blk - b0) & 1);
+    // block blk landed; block blk+1 (and the previous block's eta store) may still fly
+    if (blk + 1 >= b1) wait_vm<0>();
+    else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
+    else wait_vm<G::NOCT + 1>();
+    const double* xs = wl + buf * G::BUF;
+
+    // ---- row stage ----
+    double eta = 0.0;
+    if (irls && !(a.dbg & 8)) {
+      double e4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int u = 0; u < CPL; ++u) {
+        const int c = LPR * u + g;
+        e4[u & 3] += xs[c * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
+      }
+      eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+      if constexpr (LPR == 4) eta = xor16_sum(eta);
+      if constexpr (LPR >= 2) eta = xor32_sum(eta);
+    }
+    if (lane < NRB) {
+      const double* vv = xs + G::XB;
+      const int64_t row = blk * NRB + rl;
+      double w = 0.0, wz = 0.0;
+      if (irls) {
+        eta = eta + (a.off ? vv[2 * NRB + rl] : 0.0);
+        if (has_eta) a.eta_out[row] = eta;  // always issued (row < n_pad): keeps vmcnt exact
+      }
+      if (row < a.n && do_rows) {
+        const double y = vv[rl];
+        const double m = a.m ? vv[NRB + rl] : 1.0;
+        const double off = a.off ? vv[2 * NRB + rl] : 0.0;
+        const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
+        if (a.dbg & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+        else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
+      }
+      wl[G::OFF_W + rl] = w;
+      wl[G::OFF_W + NRB + rl] = wz;
+    }
+
+    // ---- Gramian: NRB/4 k-steps of 4 rows ----
+    if (do_gram) {
+#pragma unroll
+      for (int s = 0; s < NRB / 4; ++s) {
+        const int r = 4 * s + rq;
+        const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + NRB + r];
+        const double* base = xs + cl * NRB + (r ^ fcl);
+        double xv[P16], av[P16];
+#pragma unroll
+        for (int b = 0; b < P16; ++b) {
+          xv[b] = base[16 * NRB * b];
+          av[b] = xv[b] * wr;
+          xz[b] += xv[b] * wzr;
+        }
+        int t = 0;
+#pragma unroll
+        for (int bi = 0; bi < P16; ++bi)
+#pragma unroll
+          for (int bj = 0; bj <= bi; ++bj, ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+      }
+    }
+    // every LDS read of this buffer has returned before the DMA may overwrite it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+  }
+
+  // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
+#pragma unroll
+  for (int b = 0; b < P16; ++b) xz[b] = xor32_sum(xor16_sum(xz[b]));
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    s_dev += __shfl_xor(s_dev, o);
+    s_aux += __shfl_xor(s_aux, o);
+  }
+
+  // ---- fixed-order tree over the 8 waves in LDS: ((w0+w4)+(w2+w6)) + ((w1+w5)+(w3+w7)) ----
+  wait_vm<0>();
+  __syncthreads();
+#pragma unroll 1
+  for (int half = NWAVE / 2; half >= 1; half >>= 1) {
+    if (wv >= half && wv < 2 * half) {
+      double* reg = lds + (wv - half) * G::PSZ;
+#pragma unroll
+      for (int t = 0; t < G::T; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) reg[t * 256 + 64 * j + lane] = acc[t][j];
+      if (lane < 16) {
+#pragma unroll
+        for (int b = 0; b < P16; ++b) reg[G::T * 256 + 16 * b + lane] = xz[b];
+      }
+      if (lane == 0) {
+        reg[G::T * 256 + G::NC] = s_dev;
+        reg[G::T * 256 + G::NC + 1] = s_aux;
+      }
+    }
+    __syncthreads();
+    if (wv < half) {
+      const double* reg = lds + wv * G::PSZ;
+#pragma unroll
+      for (int t = 0; t < G::T; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] += reg[t * 256 + 64 * j + lane];
+#pragma unroll
+      for (int b = 0; b < P16; ++b) xz[b] += reg[G::T * 256 + 16 * b + (lane & 15)];
+      s_dev += reg[G::T * 256 + G::NC];
+      s_aux += reg[G::T * 256 + G::NC + 1];
+    }
+    __syncthreads();
+  }
+  if (wv == 0) {
+    double* out = a.partials + (int64_t)blockIdx.x * a.stride;
+#pragma unroll
+    for (int t = 0; t < G::T; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t][j];
+    if (lane < 16) {
+#pragma unroll
+      for (int b = 0; b < P16; ++b) out[G::T * 256 + 16 * b + lane] = xz[b];
+    }
+    if (lane < NS) out[G::T * 256 + G::NC + lane] = lane == S_DEV ? s_dev : (lane == S_SUMW ? s_aux : 0.0);
+  }
+}
+
+template <int P16>
+hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st) {
+  const dim3 gr(grid), bl(64 * NWAVE);
+  const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
+  const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), gr, bl, 0, st, a);
+  else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), gr, bl, 0, st, a);
+  else if (fam == FAM_BINOMIAL)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), gr, bl, 0, st, a);
+  else if (fam == FAM_GAUSSIAN)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), gr, bl, 0, st, a);
+  else if (fam == FAM_POISSON)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_POISSON, LNK_LOG>), gr, bl, 0, st, a);
+  else if (fam == FAM_GAMMA)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_GAMMA, LNK_INVERSE>), gr, bl, 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int narrow_variant(int p) { return (p + 15) / 16; }
+int narrow_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS; }
+int narrow_wg_per_cu() { return 1; }
+int narrow_rows_per_wg() { return 16 * NWAVE; }
+
+hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st) {
+  switch (P16) {
+    case 1: return launch_narrow_p<1>(a, grid, st);
+    case 2: return launch_narrow_p<2>(a, grid, st);
+    case 3: return launch_narrow_p<3>(a, grid, st);
+    case 4: return launch_narrow_p<4>(a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace sglm

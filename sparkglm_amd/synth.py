@@ -12,6 +12,8 @@ multiply/add only (no FMA contraction, no libm).
   kind 1 (gaussian):       y = eta* + (2 u_y - 1)
   kind 2 (poisson counts): y = floor(u_y * 2 * max(1 + 0.5 eta*, 0.1)),
                            offset = 0.1 (2 u_o - 1),  prior = 0.5 + u_p
+  kind 3 (gamma, inverse link): column j>0 is (0.5 + u) / sqrt(p) (positive), b_0 = 1,
+                           b_j = 0.1 ((j mod 5) + 1), y = (0.25 + 1.5 u_y) / eta*  (> 0)
 """
 from __future__ import annotations
 
@@ -41,7 +43,11 @@ def unif(keys):
     return (splitmix64(keys) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
 
 
-def beta_star(p: int) -> np.ndarray:
+def beta_star(p: int, kind: int = 0) -> np.ndarray:
+    if kind == 3:
+        b = np.array([0.1 * ((j % 5) + 1) for j in range(p)], dtype=np.float64)
+        b[0] = 1.0
+        return b
     b = np.array([0.5 * ((j % 5) - 2) for j in range(p)], dtype=np.float64)
     b[0] = -0.25
     return b
@@ -56,13 +62,15 @@ def generate(kind: int, row0: int, n: int, p: int, seed: int):
     gi = np.arange(row0, row0 + n, dtype=np.uint64)
     scale = 1.0 / np.sqrt(np.float64(p))
     X = np.empty((n, p), dtype=np.float64, order="F")
-    bs = beta_star(p)
+    bs = beta_star(p, kind)
     eta = np.zeros(n, dtype=np.float64)
     with np.errstate(over="ignore"):
         base = np.uint64(kx) + gi * np.uint64(p)
         for j in range(p):
             if j == 0:
                 x = np.ones(n, dtype=np.float64)
+            elif kind == 3:
+                x = (0.5 + unif(base + np.uint64(j))) * scale
             else:
                 x = (2.0 * unif(base + np.uint64(j)) - 1.0) * scale
             X[:, j] = x
@@ -80,6 +88,8 @@ def generate(kind: int, row0: int, n: int, p: int, seed: int):
             y = np.floor(u * 2.0 * lam)
             offset = (2.0 * unif(np.uint64(ko) + gi) - 1.0) * 0.1
             prior = 0.5 + unif(np.uint64(kp) + gi)
+        elif kind == 3:
+            y = (0.25 + 1.5 * u) / eta
         else:
-            raise ValueError("kind must be 0, 1 or 2")
+            raise ValueError("kind must be 0, 1, 2 or 3")
     return X, y, offset, prior

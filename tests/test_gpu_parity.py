@@ -44,7 +44,7 @@ def test_golden_cases(eng, golden):
 
 
 def test_synth_is_bit_identical_to_host_generator(eng):
-    for kind in (0, 1, 2):
+    for kind in (0, 1, 2, 3):
         for row0, n, p in ((0, 37, 5), (123456789, 1000, 20), (5, 3000, 256)):
             eng.synth(kind, row0, n, p, 99)
             X, y, m, off, pr = eng.get_data()

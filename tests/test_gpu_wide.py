@@ -177,3 +177,18 @@ def test_wide_large_properties(eng):
     g = eng.fit_glm()
     np.testing.assert_array_equal(f.coefs, g.coefs)
     np.testing.assert_array_equal(f.stderr, g.stderr)
+
+
+@pytest.mark.parametrize("p", [64, 1100])
+def test_gamma_synth_design_device_generated(eng, p):
+    """BASELINE configs[3]'s design (synth kind 3: positive X, gamma/inverse) generated in HBM by
+    the device generator; the oracle fits the bit-identical host copy."""
+    n = 9000
+    eng.synth(3, 1000, n, p, 4)
+    X, y, _, _ = synth.generate(3, 1000, n, p, 4)
+    f = eng.fit_glm("gamma", "inverse")
+    o = po.fit_glm(X, y, "gamma", "inverse", nthreads=8)
+    assert f.iter == o.iter
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
+               [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL

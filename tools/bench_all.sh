@@ -1,14 +1,22 @@
 #!/bin/bash
-# Every BASELINE config as a bench workload (1 GPU), one JSON line each -> gpurun_out/bench_<wl>.json
+# Every BASELINE config as a bench workload (1 GPU): one JSON line each -> gpurun_out/bench_<wl>.json,
+# and a rocprofv3 --kernel-trace --stats summary of the same command -> gpurun_out/prof_<wl>/
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for wl in ${WLS:-poisson64 logit512 gamma2048}; do
+export TMPDIR=/tmp
+for wl in ${WLS:-logit256 poisson64 logit512 gamma2048}; do
   steps=10; warm=2
   [[ $wl == gamma2048 ]] && { steps=3; warm=1; }
   timeout -k 10 400 python bench.py --workload $wl --steps $steps --warmup $warm > gpurun_out/bench_$wl.json 2> gpurun_out/bench_$wl.err
   rc=$?
   echo "$wl rc=$rc"; cat gpurun_out/bench_$wl.json
   [[ $rc -ne 0 ]] && { tail -20 gpurun_out/bench_$wl.err; exit $rc; }
+  if [[ -n "$PROF" ]]; then
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$wl" -o run --output-format csv -- python bench.py --workload $wl --steps $steps --warmup $warm --no-cpu-baseline > gpurun_out/prof_bench_$wl.json 2> gpurun_out/prof_bench_$wl.err
+    rc=$?
+    echo "prof $wl rc=$rc"
+    [[ $rc -ne 0 ]] && { tail -20 gpurun_out/prof_bench_$wl.err; exit $rc; }
+  fi
 done
 exit 0

@@ -1,0 +1,14 @@
+#!/bin/bash
+# PMC evidence per bench workload: HBM bytes (FETCH_SIZE, WRITE_SIZE: separate passes) and
+# clock / MFMA busy, over tools/pass_bench.py at a reduced row count (same per-row pattern).
+cd "$GRAFT_REPO_ROOT" || exit 1
+run_wl() {  # name PN PP PKIND PF PL
+  local name=$1
+  export PN=$2 PP=$3 PKIND=$4 PF=$5 PL=$6 PK=2
+  bash tools/pmc_counters.sh "$name" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" || exit 1
+}
+run_wl poisson64 50000000 64 2 poisson log
+run_wl logit256 20000000 256 0 binomial logit
+run_wl logit512 8000000 512 0 binomial logit
+run_wl gamma2048 2000000 2048 3 gamma inverse
+exit 0

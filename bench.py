@@ -29,6 +29,7 @@ sys.path.insert(0, HERE)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X fp64 matrix, dense (datasheet; equal to the fp64 vector rate)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+RIDGE = FP64_MFMA_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # ~9.8 flop/B
 METRIC = "rows/sec per IRLS iteration + time-to-converge, 1/2/4/8 MI355X"
 
 
@@ -51,6 +52,10 @@ WORKLOADS = {
                       cpu_rows=40_000,
                       label="gamma/inverse glm, 50M x 2048 wide design over 4 GPUs = 12.5M rows per GPU, "
                             "GPU Cholesky (BASELINE configs[3])"),
+    "logit1b": dict(cfg=1, kind=0, family="binomial", link="logit", p=32, rows=None, strong_rows=1_000_000_000,
+                    seed=6, cpu_rows=8_000_000,
+                    label="binomial/logit glm, 1B x 32 rows fixed and row-sharded over the N GPUs (north star: "
+                          "strong scaling of time-to-convergence on a 1B-row logistic GLM)"),
     "logit512": dict(cfg=4, kind=0, family="binomial", link="logit", p=512, rows=60_000_000, seed=5,
                      cpu_rows=300_000,
                      label="binomial/logit glm, p = 512 (BASELINE configs[4]); 2B x 512 = 8.19 TB is not "
@@ -125,13 +130,20 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
-    n = args.rows or wl["rows"]
+    strong = wl.get("strong_rows") is not None and args.rows is None
+    if strong:  # fixed global rows, contiguous shards (Spark's slicing: distributed.shard_range)
+        from sparkglm_amd.distributed import shard_range
+        lo, hi = shard_range(wl["strong_rows"], world, rank)
+        n, row0 = hi - lo, lo
+    else:
+        n = args.rows or wl["rows"]
+        row0 = rank * n
     p = args.p or wl["p"]
     seed = wl["seed"] if args.seed is None else args.seed
     fam, lnk = wl["family"], wl["link"]
     eng = Engine(local)
     t0 = time.perf_counter()
-    eng.synth(wl["kind"], rank * n, n, p, seed)  # this rank's shard of the global design
+    eng.synth(wl["kind"], row0, n, p, seed)  # this rank's shard of the global design
     gen_s = time.perf_counter() - t0
     if dist_on:
         if args.comm == "rccl":
@@ -168,7 +180,7 @@ def main() -> int:
         dt, ttc = float(tt[0]), float(tt[1])
 
     if rank == 0:
-        total_rows = n * world
+        total_rows = wl["strong_rows"] if strong else n * world
         passes = max(st["passes"], 1)
         wide = st["path"] == 1
         nvec = 1 + (2 if wl["kind"] == 2 else 0)  # y (+ offset, prior)
@@ -178,6 +190,10 @@ def main() -> int:
             kern = "wide_gram_kernel"
             kern_ms = st["gram_kernel_ms"] / passes
             pass_ms = (st["gram_kernel_ms"] + st["row_kernel_ms"]) / passes
+        elif st["path"] == 2:
+            kern = f"irls_narrow_kernel<{(p + 15) // 16},{fam},{lnk}>"
+            kern_ms = st["pass_kernel_ms"] / passes
+            pass_ms = kern_ms
         else:
             kern = f"irls_pass_kernel<{(p + 15) // 16 + ((p + 15) // 16) % 2},{fam},{lnk}>"
             kern_ms = st["pass_kernel_ms"] / passes
@@ -185,7 +201,7 @@ def main() -> int:
         tflops = flops / (kern_ms * 1e-3) / 1e12
         gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
         traffic = pmc_traffic(p, n, fam)
-        if wl["cfg"] == 2:  # HBM-bound fused pass (AI ~ 8 flop/B <= ridge)
+        if flops / bytes_pass < RIDGE:  # HBM-bound fused pass (arithmetic intensity below the ridge)
             roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": kern_ms,
                     "algorithmic_bytes_per_launch": bytes_pass,
@@ -204,7 +220,7 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded counter-based generator, generated in HBM)",

@@ -162,3 +162,17 @@ def test_large_prefix_and_properties(eng):
     assert np.max(np.abs(score)) < 1e-6 * np.max(np.abs(xz))
     g = eng.fit_glm()
     np.testing.assert_array_equal(f.coefs, g.coefs)
+
+
+def test_lm_on_model_matrix_of_mixed_fixture():
+    """modelMatrix (dummy coding of x7) -> LM.fit through the API mirror, vs the oracle."""
+    from sparkglm_amd.frame import Frame
+    from sparkglm_amd.lm import LM
+    from sparkglm_amd.model_matrix import modelMatrix
+    raw = Frame.read_json(os.path.join(GOLDEN, "linear_reg_mixed.json"))
+    mm = modelMatrix(raw.select("intercept", "x1", "x2", "x3", "x4", "x5", "x6", "x7"))
+    y = raw.select("y")
+    m = LM.fit(mm, y)
+    r = po.fit_lm(mm.to_matrix(), y.to_vector())
+    assert list(m.xnames) == mm.columns
+    assert rel(m.coefs, r["coefs"]) < TOL and rel(m.stdErr, r["stderr"]) < TOL

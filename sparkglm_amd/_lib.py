@@ -96,7 +96,7 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"sparkglm_amd: HIP engine library missing at {LIB_PATH}; "
-                          f"build it with `python -m sparkglm_amd.build`")
+                          f"build it with `make -C sparkglm_amd/csrc` (or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
     E = C.POINTER(C.c_void_p)
     h = C.c_void_p

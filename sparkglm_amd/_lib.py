@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsglm_hip.so")
+# SGLM_LIB selects another in-tree build of the same library (A/B kernel comparisons in tools/)
+LIB_PATH = os.environ.get("SGLM_LIB") or os.path.join(HERE, "lib", "libsglm_hip.so")
 
 SGLM_OK, SGLM_EINVAL, SGLM_ESINGULAR, SGLM_EHIP, SGLM_ECOMM, SGLM_ENOMEM = range(6)
 FAMILIES = {"binomial": 0, "gaussian": 1, "poisson": 2, "gamma": 3}

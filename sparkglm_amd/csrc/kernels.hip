@@ -39,14 +39,15 @@ struct Geo {
   static constexpr int NCE = (NC + 31) / 32 * 32;  // columns in the LDS image (eta stripes)
   static constexpr int T = P16 * (P16 + 1) / 2;    // lower-triangular 16x16 tiles
   static constexpr int TPW = P16 + 1;              // tiles per wave
-  static constexpr int QPW = 8;                    // X column quads DMA'd per wave per block (4*P16/NW)
-  static constexpr int VPW = NW >= 4 ? 1 : 4 / NW; // vectors (y, m, offset, prior) DMA'd per wave (w < 4)
   // The row stage runs on the "row group": waves NW/2 .. NW/2+NRW-1 (wave 0 when NW == 1),
   // one wave per SIMD, NRW a power of two, RW rows each.
   static constexpr int NRW = NW >= 8 ? 4 : (NW >= 4 ? 2 : 1);
   static constexpr int ROW0 = NW >= 2 ? NW / 2 : 0;   // first wave of the row group
   static constexpr int RW = RB / NRW;              // rows per row-group wave
   static constexpr int CPG = RW / 2;               // columns per lane group per 32-column stripe
+  static constexpr int QRW = 4 * P16 / NRW;        // X column quads DMA'd per row wave per block
+  static constexpr int VRW = 4 / NRW;              // vectors (y, m, offset, prior) DMA'd per row wave
+  static_assert((4 * P16) % NRW == 0, "quads split evenly over the row waves");
   static constexpr int XB = NCE * RB;              // doubles per X buffer
   // LDS layout, in doubles (one __shared__ array: keeps hipcc's LDS-DMA waits counted)
   static constexpr int OFF_X = 0;                  // [2][XB]
@@ -54,7 +55,8 @@ struct Geo {
   static constexpr int OFF_BETA = OFF_V + 8 * RB;  // [NCE]
   static constexpr int OFF_W = OFF_BETA + NCE;     // [2][w RB | w*z RB]
   static constexpr int OFF_RED = OFF_W + 4 * RB;   // [NW][NS]
-  static constexpr int LDS_DOUBLES = OFF_RED + NW * NS;
+  static constexpr int OFF_FLAG = OFF_RED + NW * NS; // row-wave staging counter (uint32)
+  static constexpr int LDS_DOUBLES = OFF_FLAG + 1;
   static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
   // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
   static constexpr int WG_PER_CU = (8 / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? 8 / NW : 160 * 1024 / (LDS_DOUBLES * 8);
@@ -80,48 +82,39 @@ __device__ __forceinline__ void lds_barrier() {
 // rows per half-wave) and the eta reads (RW rows x 64/RW column groups) conflict free.
 // ---------------------------------------------------------------------------------
 template <int P16>
-__device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs& a, int64_t blk, int wv,
+__device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs& a, int64_t blk, int rw,
                                             int lane) {
+  // issued by the row-group waves only: row wave rw moves quads [rw*QRW, (rw+1)*QRW) and
+  // vectors [rw*VRW, (rw+1)*VRW)
   using G = Geo<P16>;
   const int64_t r0 = blk * RB;
-  double* xdst = lds + G::OFF_X + buf * G::XB;
+  // LDS-DMA destinations in address space 3, formed from the shared array's LDS address
+  typedef __attribute__((address_space(3))) double lds_double;
+  lds_double* l3 = (lds_double*)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void*)lds);
+  lds_double* xdst = l3 + G::OFF_X + buf * G::XB;
   const int i = lane & 15, cq = lane >> 4;
   // lane part of the source address; the column-quad part is wave-uniform (SGPRs).
   const double* lbase = a.X + (int64_t)cq * a.ld + r0;
 #pragma unroll
-  for (int k = 0; k < G::QPW; ++k) {
-    const int q = wv * G::QPW + k;                             // LDS column quad
+  for (int k = 0; k < G::QRW; ++k) {
+    const int q = rw * G::QRW + k;                             // LDS column quad
     const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
     const int srow = (2 * i) ^ ((8 * q + 2 * cq) & 31);        // slot swizzle of column 4q + cq
     const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + q * 128), 16, 0, 0);
   }
-  if (wv < 4) {
 #pragma unroll
-    for (int k = 0; k < G::VPW; ++k) {
-      // vector v: 0 y, 1 m, 2 offset, 3 prior (absent vectors re-load y)
-      const int v = wv * G::VPW + k;
-      const double* src = a.y;
-      if (v == 1 && a.m) src = a.m;
-      if (v == 2 && a.off) src = a.off;
-      if (v == 3 && a.prior) src = a.prior;
-      if (lane < 16) {
-        __builtin_amdgcn_global_load_lds((const void*)(src + r0 + 2 * lane),
-                                         (lds_void*)(lds + G::OFF_V + buf * 4 * RB + v * RB), 16, 0, 0);
-      }
+  for (int k = 0; k < G::VRW; ++k) {
+    // vector v: 0 y, 1 m, 2 offset, 3 prior (absent vectors re-load y)
+    const int v = rw * G::VRW + k;
+    const double* src = a.y;
+    if (v == 1 && a.m) src = a.m;
+    if (v == 2 && a.off) src = a.off;
+    if (v == 3 && a.prior) src = a.prior;
+    if (lane < 16) {
+      __builtin_amdgcn_global_load_lds((const void*)(src + r0 + 2 * lane),
+                                       (lds_void*)(l3 + G::OFF_V + buf * 4 * RB + v * RB), 16, 0, 0);
     }
-  }
-}
-
-template <int P16>
-__device__ __forceinline__ void wait_block(int wv, bool last) {
-  using G = Geo<P16>;
-  if (last) {
-    wait_vmcnt<0>();
-  } else if (wv < 4) {
-    wait_vmcnt<G::QPW + G::VPW>();
-  } else {
-    wait_vmcnt<G::QPW>();
   }
 }
 
@@ -230,59 +223,62 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
   }
 }
 
-// Pipeline per row block i (cur = i & 1):
-//   MFMA k-steps 0-3 of block i            | DMA of block i+1 landing
-//   wait for block i+1, barrier
-//   waves <  NW/2: MFMA k 4-7 of i, then the row stage of block i+1
-//   waves >= NW/2: row stage of block i+1, then MFMA k 4-7 of i     (the two halves of a
-//                  SIMD overlap MFMA with VALU work: waves w and w+4 share a SIMD)
-//   barrier; DMA of block i+2 into the buffer block i occupied.
+// Pipeline per row block i (cur = i & 1), ONE barrier per block:
+//   MFMA-only waves:  MFMA k-steps 0-7 of block i                              | barrier
+//   row waves:        MFMA k 0-3 of i; wait for their own LDS-DMA of block i+1;
+//                     row stage of block i+1 (w, w*z); MFMA k 4-7 of i         | barrier;
+//                     LDS-DMA of block i+2 into the buffer block i occupied.
+// A wave's own LDS-DMA is complete at its vmcnt wait, so only the end-of-block barrier
+// orders the image / w buffers across waves.  The row waves carry the critical path (their
+// MFMAs + the row stage) and run at raised priority; the MFMA-only partner on the same SIMD
+// fills the gaps.
 template <int P16, int FAM, int LNK, int WV>
 __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv, int lane) {
   using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
   const bool do_gram = !(a.dbg & 2);
-  const bool early_rows = (G::NW >= 2) && (wv >= G::NW / 2);
+  const int rw = wv - G::ROW0;
+  const bool row_wave = rw >= 0 && rw < G::NRW;
+  unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
   d4 acc[P16 + 1];
 #pragma unroll
   for (int k = 0; k <= P16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
 
-  // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
-  // stage of block blk+1; one call site each keeps the register allocation flat.
-  if (b0 < b1) {
-    stage_block<P16>(lds, 0, a, b0, wv, lane);
-    if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, wv, lane);
+  if (row_wave && b0 < b1) {
+    stage_block<P16>(lds, 0, a, b0, rw, lane);
+    if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, rw, lane);
   }
+  if (row_wave) __builtin_amdgcn_s_setprio(1);
+  // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
+  // stage of block blk+1.
 #pragma unroll 1
   for (int64_t blk = b0 - 1; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);  // buffers of block blk; block blk+1 uses cur ^ 1
     const bool has_gram = blk >= b0 && do_gram;
     const bool has_next = blk + 1 < b1;
-#pragma unroll 1
-    for (int ph = 0; ph < 3; ++ph) {
-      if (ph == 1) {
-        if (blk + 2 < b1 && blk + 1 == b0) {
-          wait_block<P16>(wv, false);  // prologue: block b0 landed, b0+1 may still fly
-        } else if (has_next) {
-          wait_vmcnt<0>();
-        }
-        lds_barrier();
+    if (has_gram) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+    if (row_wave && has_next) {
+      // this wave's part of block blk+1 landed (prologue: block b0+1 may still fly behind b0)
+      if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QRW + G::VRW>();
+      else wait_vmcnt<0>();
+      // ... and every row wave's part: the row waves count landed parts in LDS (each row
+      // needs all columns; the MFMA-only waves are not held up by this)
+      if constexpr (G::NRW > 1) {
+        if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned target = (unsigned)(G::NRW * (blk + 2 - b0));
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+          __builtin_amdgcn_s_sleep(1);
       }
-      const bool rows = has_next && ((ph == 1 && early_rows) || (ph == 2 && !early_rows));
-      const bool mfma = has_gram && (ph == 0 || (ph == 1 && !early_rows) || (ph == 2 && early_rows));
-      if (mfma) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, ph == 0 ? 0 : RB / 8, acc, xz_lo, xz_hi);
-      if (rows && !(a.dbg & 1)) {
-        __builtin_amdgcn_s_setprio(1);  // the row stage is on the critical path; the partner wave's MFMAs are not
-        row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
-        __builtin_amdgcn_s_setprio(0);
-      }
+      if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
     }
+    if (has_gram) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, RB / 8, acc, xz_lo, xz_hi);
     lds_barrier();
-    if (blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, wv, lane);
+    if (row_wave && blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, rw, lane);
   }
+  if (row_wave) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue: this workgroup's partial (tile t of wave wv: see gram_steps) ----
   double* out = a.partials + (int64_t)wg * a.stride;
@@ -332,6 +328,7 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
+  if (threadIdx.x == 0) *(unsigned*)(lds + G::OFF_FLAG) = 0u;
   if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
       lds[G::OFF_X + G::NC * RB + e] = 0.0;

@@ -175,4 +175,4 @@ def test_lm_on_model_matrix_of_mixed_fixture():
     m = LM.fit(mm, y)
     r = po.fit_lm(mm.to_matrix(), y.to_vector())
     assert list(m.xnames) == mm.columns
-    assert rel(m.coefs, r["coefs"]) < TOL and rel(m.stdErr, r["stderr"]) < TOL
+    assert rel(np.ravel(m.coefs), r["coefs"]) < TOL and rel(m.stdErr, r["stderr"]) < TOL

@@ -21,6 +21,10 @@
 #include "kernels.hpp"
 #include "rowmath.hpp"
 
+#ifndef SGLM_SPLIT16
+#define SGLM_SPLIT16 19
+#endif
+
 namespace sglm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -28,8 +32,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 // ---------------------------------------------------------------------------------
 // compile-time geometry.  P16 (even) column blocks of 16; NW = P16/2 waves.  Wave w
-// owns the block rows lo = w and hi = P16-1-w of the lower-triangular tile grid:
-// tiles (lo, 0..lo) and (hi, 0..hi), i.e. P16+1 tiles per wave, for the whole launch.
+// owns the block rows lo = lo_row(w) and hi = P16-1-w of the lower-triangular tile grid:
+// tiles (lo, 0..lo) and (hi, 0..hi), lo+hi+2 tiles, for the whole launch.
 // ---------------------------------------------------------------------------------
 template <int P16>
 struct Geo {
@@ -48,7 +52,11 @@ struct Geo {
   static constexpr int QRW = 4 * P16 / NRW;        // X column quads DMA'd per row wave per block
   static constexpr int VRW = 4 / NRW;              // vectors (y, m, offset, prior) DMA'd per row wave
   static_assert((4 * P16) % NRW == 0, "quads split evenly over the row waves");
-  static constexpr int XB = NCE * RB;              // doubles per X buffer
+  // 16-column blocks of the image are BSTR = 16*RB + 1 doubles apart: the pad keeps the
+  // compiler from pairing the per-block B-operand reads into ds_read2st64_b64 (32-bank rule,
+  // 2-way conflicts under the slot swizzle, 8 LDS cycles) -- they stay ds_read_b64
+  static constexpr int BSTR = 16 * RB + 1;
+  static constexpr int XB = (NCE / 16) * BSTR;     // doubles per X buffer
   // LDS layout, in doubles (one __shared__ array: keeps hipcc's LDS-DMA waits counted)
   static constexpr int OFF_X = 0;                  // [2][XB]
   static constexpr int OFF_V = 2 * XB;             // [2][4][RB]  y, m, offset, prior
@@ -61,6 +69,37 @@ struct Geo {
   // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
   static constexpr int WG_PER_CU = (8 / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? 8 / NW : 160 * 1024 / (LDS_DOUBLES * 8);
   static constexpr int WAVES_PER_SIMD = (WG_PER_CU * NW + 3) / 4;
+  // Block rows of wave wv's tiles: HI = P16-1-wv and LO below.  The row waves carry the row
+  // stage on top of their MFMAs, so they take the LOW rows 0..NRW-1 (fewest tiles) and the
+  // first NRW MFMA-only waves take ROW0.. in exchange (P16 = 16: 13 tiles per row wave, 21
+  // per MFMA-only wave 0-3, instead of 17 everywhere).
+  // P16 = 16 uses SPLIT16 (row waves 15 / MFMA-only waves 19 tiles: a 13 / 21 split would
+  // not fit the 256-VGPR budget of two waves per SIMD).
+  static constexpr int SPLIT16 = SGLM_SPLIT16;
+  static constexpr int lo_row(int wv) {
+    if (P16 == 16 && SPLIT16 == 19) {
+      constexpr int t[8] = {2, 3, 6, 7, 0, 1, 4, 5};
+      return t[wv];
+    }
+    if (P16 == 16 && SPLIT16 == 18) {
+      constexpr int t[8] = {1, 3, 5, 7, 0, 2, 4, 6};
+      return t[wv];
+    }
+    if ((P16 == 16 && SPLIT16 == 17) || SPLIT16 == 0) return wv;  // 0: no exchange at any P16
+    return wv < NRW ? ROW0 + wv : (wv >= ROW0 && wv < ROW0 + NRW ? wv - ROW0 : wv);
+  }
+  static constexpr int hi_row(int wv) {
+    if (P16 == 16 && SPLIT16 == 19) {
+      constexpr int t[8] = {15, 14, 11, 10, 13, 12, 9, 8};
+      return t[wv];
+    }
+    if (P16 == 16 && SPLIT16 == 18) {
+      constexpr int t[8] = {15, 13, 11, 9, 14, 12, 10, 8};
+      return t[wv];
+    }
+    return P16 - 1 - wv;
+  }
+  static constexpr int ntiles(int wv) { return lo_row(wv) + hi_row(wv) + 2; }
 };
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left open (gfx9 encoding).
@@ -101,7 +140,8 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
     const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
     const int srow = (2 * i) ^ ((8 * q + 2 * cq) & 31);        // slot swizzle of column 4q + cq
     const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + q * 128), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128), 16, 0,
+                                     0);
   }
 #pragma unroll
   for (int k = 0; k < G::VRW; ++k) {
@@ -156,9 +196,9 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
 #pragma unroll
     for (int u = 0; u < G::CPG; ++u) {
       const int c0 = G::CPG * g + u;  // column in stripe 0; stripe t adds 32 columns, same slot
-      const double* base = xs + c0 * 32 + (r ^ ((2 * c0) & 31));
+      const double* base = xs + (c0 >> 4) * G::BSTR + (c0 & 15) * 32 + (r ^ ((2 * c0) & 31));
 #pragma unroll
-      for (int t = 0; t < G::NCE / 32; ++t) e4[(u * (G::NCE / 32) + t) & 3] += base[1024 * t] * beta[c0 + 32 * t];
+      for (int t = 0; t < G::NCE / 32; ++t) e4[(u * (G::NCE / 32) + t) & 3] += base[2 * G::BSTR * t] * beta[c0 + 32 * t];
     }
     eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);  // beta is 0 past p
     if constexpr (G::RW <= 8) eta = add_xor8(eta);
@@ -187,7 +227,7 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
 }
 
 // MFMA k-steps [S0, S1) of one block for wave WV (compile-time, so every operand is a
-// static LDS offset).  Wave WV owns block rows LO = WV and HI = P16-1-WV of the lower
+// static LDS offset).  Wave WV owns block rows LO = lo_row(WV) and HI = P16-1-WV of the lower
 // tile grid: tiles (LO, 0..LO) then (HI, 0..HI).  Lane l reads X[k0 + (l>>4)][16b + (l&15)];
 // the A operand (blocks LO / HI) is scaled by the lane's row weight, the B operands are
 // used straight from LDS.  X'Wz accumulates on the VALU from the same A fragments.
@@ -196,9 +236,9 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
 // k-step's MFMAs; wide variants carry enough MFMAs per k-step to cover the read latency.
 template <int P16, int WV>
 __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0,
-                                           d4 (&acc)[P16 + 1], double& xz_lo, double& xz_hi) {
+                                           d4 (&acc)[Geo<P16>::ntiles(WV)], double& xz_lo, double& xz_hi) {
   using G = Geo<P16>;
-  constexpr int LO = WV, HI = P16 - 1 - WV;
+  constexpr int LO = Geo<P16>::lo_row(WV), HI = Geo<P16>::hi_row(WV);
   constexpr int UNR = P16 <= 8 ? RB / 8 : 1;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* w = lds + G::OFF_W + wb * 2 * RB;
@@ -209,15 +249,15 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
     const int r = 4 * (S0 + j) + rq;
     const double* base = colbase + (r ^ (2 * cl));
     const double wr = w[r], wzr = w[RB + r];
-    const double x_lo = base[512 * LO], x_hi = base[512 * HI];
+    const double x_lo = base[G::BSTR * LO], x_hi = base[G::BSTR * HI];
     const double a_lo = x_lo * wr, a_hi = x_hi * wr;
     xz_lo += x_lo * wzr;
     xz_hi += x_hi * wzr;
 #pragma unroll
-    for (int k = 0; k <= P16; ++k) {
+    for (int k = 0; k < Geo<P16>::ntiles(WV); ++k) {
       constexpr int dummy = 0;
       (void)dummy;
-      const double b = base[512 * (k <= LO ? k : k - LO - 1)];
+      const double b = base[G::BSTR * (k <= LO ? k : k - LO - 1)];
       acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
     }
   }
@@ -242,9 +282,9 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   const bool row_wave = rw >= 0 && rw < G::NRW;
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
-  d4 acc[P16 + 1];
+  d4 acc[G::ntiles(WV)];
 #pragma unroll
-  for (int k = 0; k <= P16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < G::ntiles(WV); ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
 
   if (row_wave && b0 < b1) {
@@ -282,9 +322,9 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
 
   // ---- epilogue: this workgroup's partial (tile t of wave wv: see gram_steps) ----
   double* out = a.partials + (int64_t)wg * a.stride;
-  constexpr int lo = WV, hi = P16 - 1 - WV;
+  constexpr int lo = G::lo_row(WV), hi = G::hi_row(WV);
 #pragma unroll
-  for (int k = 0; k <= P16; ++k) {
+  for (int k = 0; k < G::ntiles(WV); ++k) {
     const int bi = k <= lo ? lo : hi, bj = k <= lo ? k : k - lo - 1;
     const int t = bi * (bi + 1) / 2 + bj;
 #pragma unroll
@@ -331,8 +371,9 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   if (threadIdx.x == 0) *(unsigned*)(lds + G::OFF_FLAG) = 0u;
   if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
-      lds[G::OFF_X + G::NC * RB + e] = 0.0;
-      lds[G::OFF_X + G::XB + G::NC * RB + e] = 0.0;
+      const int c = G::NC + e / RB, r = e % RB;
+      lds[G::OFF_X + (c >> 4) * G::BSTR + (c & 15) * RB + r] = 0.0;
+      lds[G::OFF_X + G::XB + (c >> 4) * G::BSTR + (c & 15) * RB + r] = 0.0;
     }
   }
   __syncthreads();

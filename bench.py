@@ -121,9 +121,17 @@ def main() -> int:
     from sparkglm_amd import Engine
 
     dist_on = world > 1
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = local % ndev  # one rank per GPU; ranks share devices only when rehearsing on fewer GPUs
+    # ranks sharing a device (rehearsing N > 1 on fewer GPUs): RCCL refuses duplicate devices,
+    # so the group is gloo and the engine all-reduces host buffers through it
+    shared = dist_on and world > ndev
     if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
 
     def barrier():
         if dist_on:
@@ -141,11 +149,14 @@ def main() -> int:
     p = args.p or wl["p"]
     seed = wl["seed"] if args.seed is None else args.seed
     fam, lnk = wl["family"], wl["link"]
-    eng = Engine(local)
+    eng = Engine(dev)
     t0 = time.perf_counter()
     eng.synth(wl["kind"], row0, n, p, seed)  # this rank's shard of the global design
     gen_s = time.perf_counter() - t0
-    if dist_on:
+    if shared:
+        from sparkglm_amd.distributed import torch_allreduce
+        eng.set_comm(torch_allreduce(), on_device=False)
+    elif dist_on:
         if args.comm == "rccl":
             uid = [Engine.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -175,7 +186,7 @@ def main() -> int:
     dt = time.perf_counter() - t0
     st = eng.stats()
     if dist_on:
-        tt = torch.tensor([dt, ttc], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt, ttc], dtype=torch.float64, device="cpu" if shared else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt, ttc = float(tt[0]), float(tt[1])
 
@@ -225,7 +236,7 @@ def main() -> int:
             "dtype": "f64",
             "data": "synthetic (seeded counter-based generator, generated in HBM)",
             "config": {"workload": wl["label"], "bench_workload": args.workload,
-                       "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}",
+                       "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}" + ("-shared-device-gloo" if shared else ""),
                        "family": fam, "link": lnk, "tol": 1e-6,
                        "offset_prior": wl["kind"] == 2},
             "time_to_converge_s": ttc,

@@ -52,10 +52,10 @@ struct Geo {
   static constexpr int QRW = 4 * P16 / NRW;        // X column quads DMA'd per row wave per block
   static constexpr int VRW = 4 / NRW;              // vectors (y, m, offset, prior) DMA'd per row wave
   static_assert((4 * P16) % NRW == 0, "quads split evenly over the row waves");
-  // 16-column blocks of the image are BSTR = 16*RB + 1 doubles apart: the pad keeps the
+  // 16-column blocks of the image are BSTR = 16*RB + 2 doubles apart: the pad keeps the
   // compiler from pairing the per-block B-operand reads into ds_read2st64_b64 (32-bank rule,
   // 2-way conflicts under the slot swizzle, 8 LDS cycles) -- they stay ds_read_b64
-  static constexpr int BSTR = 16 * RB + 1;
+  static constexpr int BSTR = 16 * RB + 2;  // (+2: keeps LDS-DMA destinations 16-B aligned)
   static constexpr int XB = (NCE / 16) * BSTR;     // doubles per X buffer
   // LDS layout, in doubles (one __shared__ array: keeps hipcc's LDS-DMA waits counted)
   static constexpr int OFF_X = 0;                  // [2][XB]

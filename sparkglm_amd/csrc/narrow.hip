@@ -57,7 +57,10 @@ struct NGeo {
   static constexpr int NOCT = NC / CPI;              // DMA wave-instructions for X per block
   static constexpr int SPER = NRB == 16 ? 2 : 16 / CPI;  // period of the swizzle over column groups
   static constexpr int LPER = NOCT < SPER ? NOCT : SPER;
-  static constexpr int XB = NC * NRB;                // doubles of X per buffer
+  // 16-column blocks BSTR = 16 NRB + 2 doubles apart: the pad keeps the per-block MFMA operand
+  // reads plain ds_read_b64 (no ds_read2st64_b64 pairing: 32-bank rule, 2-way conflicts)
+  static constexpr int BSTR = 16 * NRB + 2;         // (+2: keeps LDS-DMA destinations 16-B aligned)
+  static constexpr int XB = P16 * BSTR;              // doubles of X per buffer
   static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
   static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB]
   static constexpr int WAVE_LDS = OFF_W + 2 * NRB;   // doubles per wave
@@ -102,7 +105,8 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
   for (int o = 0; o < G::NOCT; ++o) {
     const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
     __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER]),
-                                     (lds_void*)(dst + o * 128), 16, 0, 0);
+                                     (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16,
+                                     0, 0);
   }
   if (G::NRB == 32 || lane < 2 * G::NRB)
     __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
@@ -181,7 +185,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
 #pragma unroll
       for (int u = 0; u < CPL; ++u) {
         const int c = LPR * u + g;
-        e4[u & 3] += xs[c * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
+        e4[u & 3] += xs[(c >> 4) * G::BSTR + (c & 15) * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
       }
       eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
       if constexpr (LPR == 4) eta = xor16_sum(eta);
@@ -217,7 +221,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
         double xv[P16], av[P16];
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
-          xv[b] = base[16 * NRB * b];
+          xv[b] = base[G::BSTR * b];
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }

@@ -21,6 +21,12 @@
 #include "kernels.hpp"
 #include "rowmath.hpp"
 
+#ifndef SGLM_K1
+#define SGLM_K1 4
+#endif
+#ifndef SGLM_PRIO
+#define SGLM_PRIO 1
+#endif
 #ifndef SGLM_SPLIT16
 #define SGLM_SPLIT16 19
 #endif
@@ -234,18 +240,18 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
 // A phase is RB/8 k-steps starting at S0.  Narrow variants (P16 <= 8: at most 9 MFMAs per
 // k-step) unroll the phase so the next k-step's LDS operand reads issue under the current
 // k-step's MFMAs; wide variants carry enough MFMAs per k-step to cover the read latency.
-template <int P16, int WV>
+template <int P16, int WV, int NST = RB / 8>
 __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0,
                                            d4 (&acc)[Geo<P16>::ntiles(WV)], double& xz_lo, double& xz_hi) {
   using G = Geo<P16>;
   constexpr int LO = Geo<P16>::lo_row(WV), HI = Geo<P16>::hi_row(WV);
-  constexpr int UNR = P16 <= 8 ? RB / 8 : 1;
+  constexpr int UNR = P16 <= 8 ? NST : 1;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* w = lds + G::OFF_W + wb * 2 * RB;
   const int cl = lane & 15, rq = lane >> 4;
   const double* colbase = xs + cl * 32;  // column c = 16b + cl has (2c & 31) == 2cl for every b
 #pragma unroll UNR
-  for (int j = 0; j < RB / 8; ++j) {
+  for (int j = 0; j < NST; ++j) {
     const int r = 4 * (S0 + j) + rq;
     const double* base = colbase + (r ^ (2 * cl));
     const double wr = w[r], wzr = w[RB + r];
@@ -280,6 +286,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   const bool do_gram = !(a.dbg & 2);
   const int rw = wv - G::ROW0;
   const bool row_wave = rw >= 0 && rw < G::NRW;
+  constexpr int K1 = SGLM_K1;  // MFMA k-steps of block i before the row stage of block i+1
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
   d4 acc[G::ntiles(WV)];
@@ -291,7 +298,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     stage_block<P16>(lds, 0, a, b0, rw, lane);
     if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, rw, lane);
   }
-  if (row_wave) __builtin_amdgcn_s_setprio(1);
+  if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(1);
   // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
   // stage of block blk+1.
 #pragma unroll 1
@@ -299,7 +306,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     const int cur = (int)((blk - b0) & 1);  // buffers of block blk; block blk+1 uses cur ^ 1
     const bool has_gram = blk >= b0 && do_gram;
     const bool has_next = blk + 1 < b1;
-    if (has_gram) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+    if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
     if (row_wave && has_next) {
       // this wave's part of block blk+1 landed (prologue: block b0+1 may still fly behind b0)
       if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QRW + G::VRW>();
@@ -314,7 +321,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
       }
       if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
     }
-    if (has_gram) gram_steps<P16, WV>(lds, cur & 1, cur & 1, lane, RB / 8, acc, xz_lo, xz_hi);
+    if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
     lds_barrier();
     if (row_wave && blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, rw, lane);
   }

@@ -7,7 +7,8 @@ seeded synthetic generator (sparkglm_amd.synth; bit-identical host copy).  A "st
 one IRLS iteration: the fused pass over every resident row (eta, mu, w, z, deviance and
 the X'WX / X'Wz Gramian on fp64 MFMA) + the all-reduce over ranks + the p x p solve.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload logit256|poisson64|gamma2048|logit512]
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+                  [--workload logit256|poisson64|gamma2048|logit512|logit512r|logit1b]
                   [--rows R] [--p P]
 
 N > 1 is launched by torch.distributed.run (one process per GPU); each rank holds its
@@ -56,10 +57,15 @@ WORKLOADS = {
                     seed=6, cpu_rows=8_000_000,
                     label="binomial/logit glm, 1B x 32 rows fixed and row-sharded over the N GPUs (north star: "
                           "strong scaling of time-to-convergence on a 1B-row logistic GLM)"),
-    "logit512": dict(cfg=4, kind=0, family="binomial", link="logit", p=512, rows=60_000_000, seed=5,
-                     cpu_rows=300_000,
-                     label="binomial/logit glm, p = 512 (BASELINE configs[4]); 2B x 512 = 8.19 TB is not "
-                           "HBM-resident on 8 GPUs, so each GPU holds the largest resident shard, 60M rows"),
+    "logit512": dict(cfg=4, kind=0, family="binomial", link="logit", p=512, rows=250_000_000, seed=5,
+                     cpu_rows=300_000, procedural=True,
+                     label="binomial/logit glm, 2B x 512 row-sharded over 8 GPUs = 250M rows per GPU (BASELINE "
+                           "configs[4]); 2B x 512 = 8.19 TB exceeds 8 x 288 GB of HBM, so X is procedural: "
+                           "regenerated in the pass kernels from the seeded generator, y / eta / w stored"),
+    "logit512r": dict(cfg=4, kind=0, family="binomial", link="logit", p=512, rows=60_000_000, seed=5,
+                      cpu_rows=300_000,
+                      label="binomial/logit glm, p = 512, HBM-resident X: the largest resident shard, 60M rows "
+                            "per GPU (BASELINE configs[4] at reduced rows)"),
 }
 
 
@@ -81,7 +87,7 @@ def cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
             "time_to_converge_s": dt, "iters": fit.iter}
 
 
-def pmc_traffic(p: int, n: int, family: str):
+def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
     """Per-launch HBM bytes of the dominant kernel: the per-row FETCH_SIZE + WRITE_SIZE measured
     by rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
     times the rows of this launch (the pass streams every row exactly once)."""
@@ -89,7 +95,8 @@ def pmc_traffic(p: int, n: int, family: str):
     try:
         with open(path) as f:
             tab = json.load(f)
-        e = tab.get(f"{family}:{p}", tab.get(str(p)) if family == "binomial" else None)
+        key = f"{family}:{p}" + (":proc" if procedural else "")
+        e = tab.get(key, tab.get(str(p)) if (family == "binomial" and not procedural) else None)
         return None if e is None else e["bytes_per_row"] * n
     except (OSError, ValueError, KeyError):
         return None
@@ -151,7 +158,7 @@ def main() -> int:
     fam, lnk = wl["family"], wl["link"]
     eng = Engine(dev)
     t0 = time.perf_counter()
-    eng.synth(wl["kind"], row0, n, p, seed)  # this rank's shard of the global design
+    eng.synth(wl["kind"], row0, n, p, seed, procedural=wl.get("procedural", False))  # this rank's shard
     gen_s = time.perf_counter() - t0
     if shared:
         from sparkglm_amd.distributed import torch_allreduce
@@ -211,7 +218,7 @@ def main() -> int:
             pass_ms = kern_ms
         tflops = flops / (kern_ms * 1e-3) / 1e12
         gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(p, n, fam)
+        traffic = pmc_traffic(p, n, fam, wl.get("procedural", False))
         if flops / bytes_pass < RIDGE:  # HBM-bound fused pass (arithmetic intensity below the ridge)
             roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": kern_ms,
@@ -238,7 +245,7 @@ def main() -> int:
             "config": {"workload": wl["label"], "bench_workload": args.workload,
                        "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}" + ("-shared-device-gloo" if shared else ""),
                        "family": fam, "link": lnk, "tol": 1e-6,
-                       "offset_prior": wl["kind"] == 2},
+                       "offset_prior": wl["kind"] == 2, "procedural_x": wl.get("procedural", False)},
             "time_to_converge_s": ttc,
             "iters_to_converge": fit.iter,
             "deviance": fit.deviance,

@@ -148,9 +148,16 @@ int sglm_set_data_device(sglm_engine *h, const double *dX, int64_t n, int64_t p,
                          const double *dprior);
 /* Generate this rank's row shard [row0, row0+n) of the seeded synthetic design directly
  * in HBM (bench / scale tests).  kind: 0 = logit design (y in {0,1}), 1 = gaussian (LM),
- * 2 = poisson counts + offset + prior.  Column 0 is the intercept.  Bit-identical to
- * sparkglm_amd.synth on the host. */
+ * 2 = poisson counts + offset + prior, 3 = gamma design (positive X, y > 0).  Column 0
+ * is the intercept.  Bit-identical to sparkglm_amd.synth on the host. */
 int sglm_synth(sglm_engine *h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed);
+/* Procedural shard of the same synthetic design: y (+ offset / prior for kind 2) are
+ * generated and stored, X is NOT -- the (wide-path) pass kernels regenerate every X[i, j]
+ * from the counter-based generator where they would have read it, bit-identical to the
+ * resident image of sglm_synth.  For designs larger than HBM (BASELINE configs[4]:
+ * 2B x 512 = 8.19 TB).  Fits, LM, predict and stats work as on a resident shard;
+ * sglm_get_data cannot return X. */
+int sglm_synth_procedural(sglm_engine *h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed);
 /* Copy back the resident design (tests; X col-major with ldx = n). */
 int sglm_get_data(sglm_engine *h, double *X, double *y, double *m, double *offset, double *prior);
 

@@ -1,6 +1,6 @@
 """ctypes binding of libsglm_hip.so (the C ABI declared in include/sglm.h).
 
-The library is built in-tree (sparkglm_amd/lib/) by ``python -m sparkglm_amd.build`` or
+The library is built in-tree (sparkglm_amd/lib/) by ``make -C sparkglm_amd/csrc`` or
 ``__graft_entry__.build()``.  There is no fallback: if the HIP library is missing the
 import fails loudly.
 """
@@ -24,7 +24,7 @@ S_DEV, S_PEARSON, S_LL, S_BAD, S_AUX0, S_AUX1, S_AUX2, S_SUMW = range(8)
 # Symbols include/sglm.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "sglm_abi_version", "sglm_last_error", "sglm_device_count", "sglm_create", "sglm_destroy",
-    "sglm_set_data", "sglm_set_data_device", "sglm_synth", "sglm_get_data", "sglm_set_comm",
+    "sglm_set_data", "sglm_set_data_device", "sglm_synth", "sglm_synth_procedural", "sglm_get_data", "sglm_set_comm",
     "sglm_rccl_unique_id", "sglm_set_comm_rccl", "sglm_fit_glm", "sglm_fit_lm", "sglm_irls_pass",
     "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
     "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
@@ -111,6 +111,7 @@ def load():
         "sglm_set_data_device": ([h, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p], C.c_int),
         "sglm_synth": ([h, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64], C.c_int),
+        "sglm_synth_procedural": ([h, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64], C.c_int),
         "sglm_get_data": ([h, dp, dp, dp, dp, dp], C.c_int),
         "sglm_set_comm": ([h, ALLREDUCE_FN, C.c_void_p, C.c_int], C.c_int),
         "sglm_rccl_unique_id": ([C.c_void_p], C.c_int),
@@ -137,6 +138,8 @@ def load():
         "sglm_pval_t": ([C.c_double, C.c_double], C.c_double),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("SGLM_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B comparison (tools/ab.py)
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res

@@ -54,6 +54,15 @@ struct PassArgs {
 constexpr int WIDE_PANEL = 128;  // columns per Gram panel (8 tile blocks of 16)
 constexpr int MAX_P_WIDE = 8192;
 
+// Procedural design (sglm_synth_procedural): X is regenerated in the kernels, never stored.
+struct ProcX {
+  int on;               // 0: X is the resident image
+  int kind, p;
+  int64_t row0, n;      // global row of local row 0; valid rows
+  uint64_t kx;          // splitmix64(seed)
+  double scale;         // 1/sqrt(p)
+};
+
 struct WideRowArgs {
   const double* X;
   int64_t ld;
@@ -70,6 +79,7 @@ struct WideRowArgs {
   double* wz;           // [n_pad] w * z
   double* eta_out;      // optional [n]
   double* row_partials; // [grid][NS]
+  ProcX proc;
 };
 
 // One run of consecutive 16-row blocks of one super-tile, processed by one workgroup of
@@ -92,6 +102,7 @@ struct WideGramArgs {
   double* partials;     // [slots][stride]
   int64_t stride;
   int dbg;              // profiling ablations: 4 DMA, 32 barriers
+  ProcX proc;
 };
 
 // Arguments of the final-statistics pass (stats_kernel).

@@ -85,6 +85,8 @@ struct sglm_engine : public Backend {
   bool wide = false, force_wide = false;
   // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; SGLM_NARROW=0 disables
   bool narrow = false, allow_narrow = true;
+  // procedural shard (sglm_synth_procedural): X regenerated in the wide kernels, not stored
+  ProcX procx{};
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
   int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
@@ -107,6 +109,7 @@ struct sglm_engine : public Backend {
       *ptr = nullptr;
     }
     n = p = n_pad = nblocks = 0;
+    procx = ProcX{};
   }
   void release() {
     (void)hipSetDevice(device);
@@ -320,7 +323,7 @@ struct sglm_engine : public Backend {
     return SGLM_OK;
   }
 
-  int alloc_data(int64_t n_, int64_t p_, bool has_m, bool has_off, bool has_prior) {
+  int alloc_data(int64_t n_, int64_t p_, bool has_m, bool has_off, bool has_prior, bool proc = false) {
     HIPCHK(hipSetDevice(device));
     free_data();
     if (n_ < 0 || p_ <= 0) {
@@ -333,18 +336,21 @@ struct sglm_engine : public Backend {
     }
     n = n_;
     p = p_;
-    wide = force_wide || p > 16 * MAX_P16;
+    wide = force_wide || proc || p > 16 * MAX_P16;
     nblocks = (n + RB - 1) / RB;
     n_pad = std::max<int64_t>(nblocks, 1) * RB;
     const size_t vb = sizeof(double) * (size_t)n_pad;
     const size_t ncols = (size_t)((p + 7) / 8 * 8);  // whole column octets for the LDS-DMA staging
-    hipError_t e = hipMalloc(&dX, vb * ncols);
-    if (e != hipSuccess) {
-      set_error(hip_msg(e, "hipMalloc(X)"));
-      free_data();
-      return SGLM_ENOMEM;
+    hipError_t e = hipSuccess;
+    if (!proc) {
+      e = hipMalloc(&dX, vb * ncols);
+      if (e != hipSuccess) {
+        set_error(hip_msg(e, "hipMalloc(X)"));
+        free_data();
+        return SGLM_ENOMEM;
+      }
+      HIPCHK(hipMemsetAsync(dX, 0, vb * ncols, st));
     }
-    HIPCHK(hipMemsetAsync(dX, 0, vb * ncols, st));
     for (auto pr : {std::make_pair(&dy, true), std::make_pair(&dm, has_m), std::make_pair(&doff, has_off),
                     std::make_pair(&dprior, has_prior), std::make_pair(&deta, true), std::make_pair(&dw, wide),
                     std::make_pair(&dwz, wide)}) {
@@ -429,6 +435,7 @@ struct sglm_engine : public Backend {
       r.wz = dwz;
       r.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
       r.row_partials = drp;
+      r.proc = procx;
       HIPCHK(launch_wide_rows(r, rgrid, st));
       HIPCHK(hipEventRecord(evm, st));
       WideGramArgs g{};
@@ -440,6 +447,7 @@ struct sglm_engine : public Backend {
       g.partials = dgp;
       g.stride = wstride;
       g.dbg = dbg;
+      g.proc = procx;
       for (int kind = 0; kind < 2; ++kind) {
         if (!has_sched[kind]) continue;
         g.pieces = dpieces[kind];
@@ -509,7 +517,7 @@ struct sglm_engine : public Backend {
     if (mode == MODE_LM_RESID) {  // pred = X * coefs into the eta buffer
       std::memcpy(hbeta, beta, sizeof(double) * p);
       HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * p, hipMemcpyHostToDevice, st));
-      HIPCHK(launch_predict(dX, n_pad, (int)p, n, dbeta, nullptr, deta, st));
+      HIPCHK(launch_predict(dX, n_pad, (int)p, n, dbeta, nullptr, deta, st, procx));
     }
     StatsArgs a{};
     a.y = dy;
@@ -810,8 +818,35 @@ int sglm_synth(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uin
   return SGLM_OK;
 }
 
+int sglm_synth_procedural(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed) {
+  if (int rc = check_handle(h)) return rc;
+  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
+    set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
+    return SGLM_EINVAL;
+  }
+  int rc = h->alloc_data(n, p, false, kind == 2, kind == 2, true);
+  if (rc) return rc;
+  const double scale = 1.0 / std::sqrt((double)p);
+  // y (and offset / prior) from the same generator; X itself is not stored
+  HIPCHK(launch_synth(kind, row0, n, (int)p, seed, scale, nullptr, h->n_pad, h->dy, nullptr, h->doff, h->dprior,
+                      h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->procx.on = 1;
+  h->procx.kind = kind;
+  h->procx.p = (int)p;
+  h->procx.row0 = row0;
+  h->procx.n = n;
+  h->procx.kx = splitmix64_host(seed);
+  h->procx.scale = scale;
+  return SGLM_OK;
+}
+
 int sglm_get_data(sglm_engine* h, double* X, double* y, double* m, double* offset, double* prior) {
   if (int rc = check_handle(h)) return rc;
+  if (X && h->procx.on) {
+    set_error("requirement failed: a procedural shard stores no X");
+    return SGLM_EINVAL;
+  }
   HIPCHK(hipSetDevice(h->device));
   const size_t vb = sizeof(double) * (size_t)h->n;
   if (X)
@@ -949,7 +984,8 @@ int sglm_predict(sglm_engine* h, const double* beta, int add_offset, double* out
   HIPCHK(hipSetDevice(h->device));
   std::memcpy(h->hbeta, beta, sizeof(double) * h->p);
   HIPCHK(hipMemcpyAsync(h->dbeta, h->hbeta, sizeof(double) * h->p, hipMemcpyHostToDevice, h->st));
-  HIPCHK(launch_predict(h->dX, h->n_pad, (int)h->p, h->n, h->dbeta, add_offset ? h->doff : nullptr, h->deta, h->st));
+  HIPCHK(launch_predict(h->dX, h->n_pad, (int)h->p, h->n, h->dbeta, add_offset ? h->doff : nullptr, h->deta, h->st,
+                        h->procx));
   HIPCHK(hipMemcpyAsync(out, h->deta, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   return SGLM_OK;

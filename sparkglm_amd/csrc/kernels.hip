@@ -19,6 +19,7 @@
 
 #include "common.hpp"
 #include "kernels.hpp"
+#include "procx.hpp"
 #include "rowmath.hpp"
 
 #ifndef SGLM_K1
@@ -431,10 +432,13 @@ __global__ void reduce_partials_kernel(const double* __restrict__ part, int64_t 
 // ---------------------------------------------------------------------------------
 __global__ void predict_kernel(const double* __restrict__ X, int64_t ld, int p, int64_t n,
                                const double* __restrict__ beta, const double* __restrict__ off,
-                               double* __restrict__ out) {
+                               double* __restrict__ out, ProcX g) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.0;
-    for (int j = 0; j < p; ++j) s += X[(int64_t)j * ld + i] * beta[j];
+    if (g.on)
+      for (int j = 0; j < p; ++j) s += proc_x(g, i, j) * beta[j];
+    else
+      for (int j = 0; j < p; ++j) s += X[(int64_t)j * ld + i] * beta[j];
     out[i] = off ? s + off[i] : s;
   }
 }
@@ -483,14 +487,6 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // ---------------------------------------------------------------------------------
 // Seeded synthetic design (bit-identical to sparkglm_amd/synth.py; no FMA contraction).
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  uint64_t z = x + 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-__device__ __forceinline__ double unif(uint64_t key) { return (double)(splitmix64(key) >> 11) * 0x1.0p-53; }
-
 __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X,
                              int64_t ld, double* y, double* m, double* off, double* prior) {
 #pragma clang fp contract(off)
@@ -500,15 +496,8 @@ __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t 
     const uint64_t gi = (uint64_t)(row0 + i);
     double eta = 0.0;
     for (int j = 0; j < p; ++j) {
-      double x;
-      if (j == 0) {
-        x = 1.0;
-      } else if (kind == 3) {  // positive design: eta > 0 for the inverse link
-        x = (0.5 + unif(kx + gi * (uint64_t)p + (uint64_t)j)) * scale;
-      } else {
-        x = (2.0 * unif(kx + gi * (uint64_t)p + (uint64_t)j) - 1.0) * scale;
-      }
-      X[(int64_t)j * ld + i] = x;
+      const double x = gen_x(kind, kx, gi, p, j, scale);  // kind 3: positive design (eta > 0)
+      if (X) X[(int64_t)j * ld + i] = x;                  // procedural shards keep only y
       double bj;
       if (kind == 3) bj = (j == 0) ? 1.0 : 0.1 * (double)((j % 5) + 1);
       else bj = (j == 0) ? -0.25 : 0.5 * (double)((j % 5) - 2);
@@ -615,17 +604,24 @@ hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, 
 }
 
 hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
-                          double* out, hipStream_t st) {
+                          double* out, hipStream_t st, const ProcX& g) {
   int64_t blocks = (n + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, ld, p, n, beta, off, out);
+  hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, ld, p, n, beta, off, out, g);
   return hipGetLastError();
 }
 
 hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hipStream_t st) {
   hipLaunchKernelGGL(ysum_kernel, dim3(nparts), dim3(256), 0, st, y, n, part);
   return hipGetLastError();
+}
+
+uint64_t splitmix64_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
 }
 
 hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,

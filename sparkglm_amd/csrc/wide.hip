@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "kernels.hpp"
+#include "procx.hpp"
 #include "rowmath.hpp"
 
 namespace sglm {
@@ -65,24 +66,36 @@ __device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
 // per-lane offsets (column within the octet, swizzled row pair; swz depends only on the
 // octet's parity), so no per-octet addresses stay live in VGPRs.  Octets past the stored
 // columns (a multiple of 8) are skipped: they only feed tiles beyond p.
-template <bool DIAG>
+// PROC: the octet is generated (procx.hpp) and written by ds_write_b128 into the slots the
+// DMA would fill (the pipeline's lgkmcnt(0) + barrier orders it like the DMA's vmcnt wait).
+template <bool DIAG, bool PROC, int K0 = 0, int K1 = (DIAG ? 4 : 8)>
 __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs& a, int64_t blk, int I, int J, int wv,
                                        const int64_t (&loff)[2], int lane) {
-  constexpr int OW = DIAG ? 4 : 8;  // octets per wave
+  constexpr int OW = DIAG ? 4 : 8;  // octets per wave; this call stages octets [K0, K1)
   const double* xb = a.X + blk * WRB;
 #pragma unroll
-  for (int k = 0; k < OW; ++k) {
+  for (int k = K0; k < K1; ++k) {
     const int qq = wv * OW + k;  // 0..15 panel I, 16..31 panel J
     const int ps = qq >> 4, ol = qq & 15;
     const int c0 = (ps ? J : I) * PANEL + ol * 8;  // first column of the octet (uniform)
-    if (c0 < a.ncols)
-      __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
-                                       (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16, 0, 0);
+    if (c0 < a.ncols) {
+      if constexpr (PROC) {
+        const int oc = lane >> 3, i = lane & 7;
+        const int64_t r = blk * WRB + ((2 * i) ^ swz(8 * (ol & 1) + oc));
+        const double2 v = {proc_x(a.proc, r, c0 + oc), proc_x(a.proc, r + 1, c0 + oc)};
+        *(double2*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128 + 2 * lane) = v;
+      } else {
+        __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
+                                         (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16, 0, 0);
+      }
+    }
   }
-  const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
-  const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
-  if (lane < WRB / 2)
-    __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
+  if (K0 == 0) {
+    const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
+    const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
+    if (lane < WRB / 2)
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
+  }
 }
 
 // Per-lane DMA offsets (doubles) for even / odd octets: column oc = lane >> 3 of the octet,
@@ -96,7 +109,11 @@ __device__ __forceinline__ void lane_offsets(const WideGramArgs& a, int lane, in
 // Off-diagonal super-tile: wave wv owns tile rows 4(wv>>1)+{0..3} of panel I and tile
 // columns 4(wv&1)+{0..3} of panel J (16 tiles).  A = X_I * w (row-scaled), B = X_J.  The
 // operands of k-step s+1 are read from LDS while the 16 MFMAs of step s issue.
-__device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[16]) {
+// hook(s) runs after the MFMAs of k-step s are issued (the procedural mode generates the next
+// block's octets there, so the integer hashing interleaves with the MFMA stream).
+template <typename Hook>
+__device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv, int lane, d4 (&acc)[16],
+                                              Hook&& hook) {
   const int cl = lane & 15, rq = lane >> 4;
   const int f = 2 * (cl >> 1);
   const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB + TB * (4 * (wv >> 1));
@@ -125,6 +142,7 @@ __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         acc[4 * t + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[t], bv[cur][u], acc[4 * t + u], 0, 0, 0);
+    hook(s);
   }
 }
 
@@ -161,7 +179,7 @@ __device__ __forceinline__ void diag_block(const double* lds, int buf, int lane,
 //   every wave is done reading the other buffer); DMA block blk+1 into the other buffer;
 //   MFMAs of block blk.  The DMA of blk+1 flies under blk's MFMAs, and the second
 //   workgroup on the CU covers whatever latency is left.
-template <int Q>
+template <int Q, bool PROC>
 __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int wv, int lane,
                            double* out) {
   d4 acc[9];
@@ -170,13 +188,13 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
   double xz_lo = 0.0, xz_hi = 0.0;
   int64_t loff[2];
   lane_offsets(a, lane, loff);
-  wstage<true>(lds, 0, a, b0, I, I, wv, loff, lane);
+  wstage<true, PROC>(lds, 0, a, b0, I, I, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
     wait_vm<0>();
     lds_bar();
-    if (blk + 1 < b1) wstage<true>(lds, cur ^ 1, a, blk + 1, I, I, wv, loff, lane);
+    if (blk + 1 < b1) wstage<true, PROC>(lds, cur ^ 1, a, blk + 1, I, I, wv, loff, lane);
     diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
   }
   constexpr int LO = Q, HI = PT - 1 - Q;
@@ -197,6 +215,7 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
   }
 }
 
+template <bool PROC>
 __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int wv,
                               int lane, double* out) {
   d4 acc[16];
@@ -205,14 +224,25 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   const int dbg = a.dbg;
   int64_t loff[2];
   lane_offsets(a, lane, loff);
-  wstage<false>(lds, 0, a, b0, I, J, wv, loff, lane);
+  wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int cur = (int)((blk - b0) & 1);
     wait_vm<0>();
     if (!(dbg & 32)) lds_bar();
-    if (blk + 1 < b1 && (!(dbg & 4) || blk == b0)) wstage<false>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-    offdiag_block(lds, cur, wv, lane, acc);
+    const bool next = blk + 1 < b1 && (!(dbg & 4) || blk == b0);
+    if constexpr (PROC) {  // generate block blk+1 two octets per k-step, under the MFMAs
+      offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
+        if (!next) return;
+        if (s == 0) wstage<false, true, 0, 2>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 1) wstage<false, true, 2, 4>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 2) wstage<false, true, 4, 6>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 3) wstage<false, true, 6, 8>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+      });
+    } else {
+      if (next) wstage<false, false>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+      offdiag_block(lds, cur, wv, lane, acc, [](int) {});
+    }
   }
   const int tr0 = 4 * (wv >> 1), tc0 = 4 * (wv & 1);
 #pragma unroll
@@ -230,7 +260,7 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
 // Persistent Gram kernels (one for the off-diagonal, one for the diagonal super-tiles, so
 // each gets the whole register file): workgroup g runs the pieces [wg_begin[g],
 // wg_begin[g+1]) of the cost-balanced schedule built on the host (engine.cpp).
-template <bool DIAG>
+template <bool DIAG, bool PROC>
 __global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a) {
   __shared__ double lds[LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
@@ -245,13 +275,13 @@ __global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a
     const int J = st - I * (I + 1) / 2;
     double* out = a.partials + (int64_t)pz.slot * a.stride;
     if constexpr (!DIAG) {
-      offdiag_piece(lds, a, I, J, pz.b0, pz.b1, wv, lane, out);
+      offdiag_piece<PROC>(lds, a, I, J, pz.b0, pz.b1, wv, lane, out);
     } else {
       switch (wv) {
-        case 0: diag_piece<0>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        case 1: diag_piece<1>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        case 2: diag_piece<2>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        default: diag_piece<3>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 0: diag_piece<0, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 1: diag_piece<1, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 2: diag_piece<2, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        default: diag_piece<3, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
       }
     }
     lds_bar();  // every wave is done with both buffers before the next piece stages
@@ -269,8 +299,19 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
     double eta = 0.0;
     if (a.mode == MODE_IRLS) {
       double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
+      if (a.proc.on) {  // procedural design: same partial-sum order as the resident image
+        int j = 0;
+        for (; j + 4 <= a.p; j += 4) {
+          e0 += proc_x(a.proc, i, j) * a.beta[j];
+          e1 += proc_x(a.proc, i, j + 1) * a.beta[j + 1];
+          e2 += proc_x(a.proc, i, j + 2) * a.beta[j + 2];
+          e3 += proc_x(a.proc, i, j + 3) * a.beta[j + 3];
+        }
+        for (; j < a.p; ++j) e0 += proc_x(a.proc, i, j) * a.beta[j];
+        eta = (e0 + e1) + (e2 + e3);
+      }
       const double* xc = a.X + i;
-      int j = 0;
+      int j = a.proc.on ? a.p : 0;
 #pragma unroll 2
       for (; j + 4 <= a.p; j += 4) {
         e0 += xc[(int64_t)j * a.ld] * a.beta[j];
@@ -279,7 +320,7 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
         e3 += xc[(int64_t)(j + 3) * a.ld] * a.beta[j + 3];
       }
       for (; j < a.p; ++j) e0 += xc[(int64_t)j * a.ld] * a.beta[j];
-      eta = (e0 + e1) + (e2 + e3);
+      if (!a.proc.on) eta = (e0 + e1) + (e2 + e3);
     }
     double w = 0.0, wz = 0.0;
     if (i < a.n) {
@@ -394,10 +435,14 @@ hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st) {
 int wide_gram_wg_per_cu() { return 2; }
 
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st) {
-  if (diag)
-    hipLaunchKernelGGL(wide_gram_kernel<true>, dim3(grid), dim3(64 * NWAVE), 0, st, a);
+  if (diag && a.proc.on)
+    hipLaunchKernelGGL((wide_gram_kernel<true, true>), dim3(grid), dim3(64 * NWAVE), 0, st, a);
+  else if (diag)
+    hipLaunchKernelGGL((wide_gram_kernel<true, false>), dim3(grid), dim3(64 * NWAVE), 0, st, a);
+  else if (a.proc.on)
+    hipLaunchKernelGGL((wide_gram_kernel<false, true>), dim3(grid), dim3(64 * NWAVE), 0, st, a);
   else
-    hipLaunchKernelGGL(wide_gram_kernel<false>, dim3(grid), dim3(64 * NWAVE), 0, st, a);
+    hipLaunchKernelGGL((wide_gram_kernel<false, false>), dim3(grid), dim3(64 * NWAVE), 0, st, a);
   return hipGetLastError();
 }
 

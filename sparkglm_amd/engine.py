@@ -116,9 +116,12 @@ class Engine:
         self.n, self.p = n, p
         return self
 
-    def synth(self, kind: int, row0: int, n: int, p: int, seed: int):
-        L.check(self._lib.sglm_synth(self._h, int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1))),
-                "sglm_synth")
+    def synth(self, kind: int, row0: int, n: int, p: int, seed: int, procedural: bool = False):
+        """Rows [row0, row0+n) of the seeded synthetic design generated in HBM.  procedural=True
+        stores y (+ offset / prior) only and regenerates X inside the kernels (wide path)."""
+        fn = self._lib.sglm_synth_procedural if procedural else self._lib.sglm_synth
+        L.check(fn(self._h, int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1))),
+                "sglm_synth_procedural" if procedural else "sglm_synth")
         self.n, self.p = n, p
         return self
 

@@ -192,3 +192,39 @@ def test_gamma_synth_design_device_generated(eng, p):
     assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
     assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
                [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL
+
+
+@pytest.mark.parametrize("kind,p,fam,link", [(0, 300, "binomial", "logit"), (2, 290, "poisson", "log"),
+                                             (3, 520, "gamma", "inverse"), (0, 40, "binomial", "logit")])
+def test_procedural_shard_is_bitwise_the_resident_fit(eng, kind, p, fam, link):
+    """sglm_synth_procedural (X regenerated in the kernels, never stored) gives bit-for-bit the
+    fit of the resident image of the same generator, and both match the oracle."""
+    n, row0 = 7000, 12345
+    eng.synth(kind, row0, n, p, 8)
+    res = eng.fit_glm(fam, link)
+    res_pred = eng.predict(res.coefs)
+    eng.synth(kind, row0, n, p, 8, procedural=True)
+    st = eng.stats()
+    assert st["path"] == 1  # procedural shards run the wide kernels at any p
+    pro = eng.fit_glm(fam, link)
+    if p > 256:  # both run the wide kernels: bit-for-bit
+        np.testing.assert_array_equal(pro.coefs, res.coefs)
+        np.testing.assert_array_equal(pro.stderr, res.stderr)
+        assert (pro.deviance, pro.pearson, pro.loglik, pro.iter) == (res.deviance, res.pearson, res.loglik, res.iter)
+        np.testing.assert_array_equal(eng.predict(pro.coefs), res_pred)
+    else:  # resident p <= 256 runs the fused/narrow pass: another summation order
+        assert pro.iter == res.iter and rel(pro.coefs, res.coefs) < 1e-12 and rel(pro.stderr, res.stderr) < 1e-12
+    X, y, off, pr = synth.generate(kind, row0, n, p, 8)
+    kw = dict(offset=off, prior=pr) if kind == 2 else {}
+    o = po.fit_glm(X, y, fam, link, nthreads=8, **kw)
+    assert pro.iter == o.iter and rel(pro.coefs, o.coefs) < TOL and rel(pro.stderr, o.stderr) < TOL
+
+
+def test_procedural_lm_and_get_data(eng):
+    eng.synth(1, 0, 6000, 300, 9, procedural=True)
+    f = eng.fit_lm()
+    X, y, _, _ = synth.generate(1, 0, 6000, 300, 9)
+    r = po.fit_lm(X, y, nthreads=8)
+    assert rel(f.coefs, r["coefs"]) < TOL and rel(f.stderr, r["stderr"]) < TOL
+    with pytest.raises(Exception):
+        eng.get_data()

@@ -8,7 +8,7 @@ n, p, k = int(os.environ.get("PN", "20000000")), int(os.environ.get("PP", "256")
 kind = int(os.environ.get("PKIND", "0"))
 fam, lnk = os.environ.get("PF", "binomial"), os.environ.get("PL", "logit")
 e = Engine(0)
-e.synth(kind, 0, n, p, 2)
+e.synth(kind, 0, n, p, 2, procedural=os.environ.get("PPROC", "0") == "1")
 b = np.full(p, 0.01)
 for _ in range(k):
     e.irls_pass(b, family=fam, link=lnk)

@@ -176,3 +176,41 @@ def test_lm_on_model_matrix_of_mixed_fixture():
     r = po.fit_lm(mm.to_matrix(), y.to_vector())
     assert list(m.xnames) == mm.columns
     assert rel(np.ravel(m.coefs), r["coefs"]) < TOL and rel(m.stdErr, r["stderr"]) < TOL
+
+
+@pytest.mark.parametrize("p,fam,link,kind", [(200, "binomial", "probit", 0), (100, "poisson", "log", 2),
+                                             (250, "gamma", "inverse", 3), (64, "gamma", "inverse", 3),
+                                             (20, "poisson", "log", 2), (180, "binomial", "cloglog", 0),
+                                             (256, "poisson", "log", 2)])
+def test_family_kernel_variants_match_oracle(eng, p, fam, link, kind):
+    """Every family / link through the fused (65 <= p <= 256) and narrow (p <= 64) kernels,
+    incl. the Poisson / Gamma row fast paths, with offset + prior where the design has them."""
+    n = 16000 if p <= 100 else 9000
+    X, y, off, pr = synth.generate(kind, 0, n, p, 2000 + p)
+    if link == "cloglog":
+        y = (synth.unif(np.arange(n, dtype=np.uint64) + np.uint64(78)) < 0.3).astype(float)
+    eng.set_data(X, y, offset=off, prior=pr)
+    f = eng.fit_glm(fam, link)
+    kw = dict(offset=off, prior=pr) if kind == 2 else {}
+    o = po.fit_glm(X, y, fam, link, nthreads=8, **kw)
+    assert f.iter == o.iter
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik], [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL
+
+
+def test_binomial_trials_m_greater_than_one(eng):
+    """m > 1 (grouped binomial, GLM.scala:483 / 580 default m = 1 overridden): y successes of m
+    trials, through the narrow and the fused kernels."""
+    for p in (30, 150):
+        n = 12000
+        X, _, _, _ = synth.generate(0, 0, n, p, 3000 + p)
+        m = 1.0 + np.floor(synth.unif(np.arange(n, dtype=np.uint64) + np.uint64(5)) * 5.0)
+        u = synth.unif(np.arange(n, dtype=np.uint64) + np.uint64(6))
+        y = np.floor(u * (m + 1.0))
+        y = np.minimum(y, m)
+        eng.set_data(X, y, m=m)
+        f = eng.fit_glm("binomial", "logit")
+        o = po.fit_glm(X, y, "binomial", "logit", m=m, nthreads=8)
+        assert f.iter == o.iter, p
+        assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL, p
+        assert rel([f.deviance, f.pearson, f.loglik], [o.deviance, o.pearson, o.loglik]) < TOL, p

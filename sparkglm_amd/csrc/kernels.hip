@@ -23,13 +23,34 @@
 #include "rowmath.hpp"
 
 #ifndef SGLM_K1
-#define SGLM_K1 4
+#define SGLM_K1 6
+#endif
+#ifndef SGLM_KA
+#define SGLM_KA 2
 #endif
 #ifndef SGLM_PRIO
 #define SGLM_PRIO 1
 #endif
 #ifndef SGLM_SPLIT16
 #define SGLM_SPLIT16 19
+#endif
+
+#ifdef SGLM_STAMPS
+// Diagnostic build only (tools/stamps.py): per-phase s_memtime stamps of workgroup 0's waves
+// over 16 steady-state blocks.  [wave 8][block 16][event 8]
+__device__ unsigned long long sglm_stamp_buf[8 * 16 * 8];
+#define SGLM_STAMP(ev)                                                                          \
+  do {                                                                                          \
+    if (blockIdx.x == 0 && blk >= b0 + 100 && blk < b0 + 116 && lane == 0)                      \
+      sglm_stamp_buf[(wv * 16 + (int)(blk - b0 - 100)) * 8 + (ev)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+extern "C" int sglm_debug_stamps(unsigned long long* out, long count) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_stamp_buf), sizeof(unsigned long long) * count);
+}
+#else
+#define SGLM_STAMP(ev) \
+  do {                 \
+  } while (0)
 #endif
 
 namespace sglm {
@@ -56,9 +77,12 @@ struct Geo {
   static constexpr int ROW0 = NW >= 2 ? NW / 2 : 0;   // first wave of the row group
   static constexpr int RW = RB / NRW;              // rows per row-group wave
   static constexpr int CPG = RW / 2;               // columns per lane group per 32-column stripe
-  static constexpr int QRW = 4 * P16 / NRW;        // X column quads DMA'd per row wave per block
-  static constexpr int VRW = 4 / NRW;              // vectors (y, m, offset, prior) DMA'd per row wave
-  static_assert((4 * P16) % NRW == 0, "quads split evenly over the row waves");
+  // LDS-DMA issuers: the MFMA-only waves (NA of them), which have slack at the block barrier;
+  // a single-wave workgroup (P16 = 2) stages its own blocks.
+  static constexpr int NA = NW - NRW;
+  static constexpr int NI = NA > 0 ? NA : 1;
+  static constexpr int QMAX = (4 * P16 + NI - 1) / NI;  // quads per issuer (at most)
+  static constexpr int VMAX = NI >= 4 ? 1 : 4 / NI;     // vectors per issuer (at most)
   // 16-column blocks of the image are BSTR = 16*RB + 2 doubles apart: the pad keeps the
   // compiler from pairing the per-block B-operand reads into ds_read2st64_b64 (32-bank rule,
   // 2-way conflicts under the slot swizzle, 8 LDS cycles) -- they stay ds_read_b64
@@ -128,11 +152,12 @@ __device__ __forceinline__ void lds_barrier() {
 // rows per half-wave) and the eta reads (RW rows x 64/RW column groups) conflict free.
 // ---------------------------------------------------------------------------------
 template <int P16>
-__device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs& a, int64_t blk, int rw,
+__device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs& a, int64_t blk, int si,
                                             int lane) {
-  // issued by the row-group waves only: row wave rw moves quads [rw*QRW, (rw+1)*QRW) and
-  // vectors [rw*VRW, (rw+1)*VRW)
+  // issuer si of NI moves quads [si*Q/NI, (si+1)*Q/NI) (Q = 4*P16) and its share of the
+  // vectors y, m, offset, prior
   using G = Geo<P16>;
+  constexpr int Q = 4 * P16;
   const int64_t r0 = blk * RB;
   // LDS-DMA destinations in address space 3, formed from the shared array's LDS address
   typedef __attribute__((address_space(3))) double lds_double;
@@ -141,9 +166,11 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
   const int i = lane & 15, cq = lane >> 4;
   // lane part of the source address; the column-quad part is wave-uniform (SGPRs).
   const double* lbase = a.X + (int64_t)cq * a.ld + r0;
+  const int q0 = si * Q / G::NI, q1 = (si + 1) * Q / G::NI;
 #pragma unroll
-  for (int k = 0; k < G::QRW; ++k) {
-    const int q = rw * G::QRW + k;                             // LDS column quad
+  for (int k = 0; k < G::QMAX; ++k) {
+    const int q = q0 + k;                                      // LDS column quad
+    if (q >= q1) break;
     const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
     const int srow = (2 * i) ^ ((8 * q + 2 * cq) & 31);        // slot swizzle of column 4q + cq
     const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
@@ -151,9 +178,10 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
                                      0);
   }
 #pragma unroll
-  for (int k = 0; k < G::VRW; ++k) {
+  for (int k = 0; k < G::VMAX; ++k) {
     // vector v: 0 y, 1 m, 2 offset, 3 prior (absent vectors re-load y)
-    const int v = rw * G::VRW + k;
+    const int v = si * G::VMAX + k;
+    if (v >= 4) break;
     const double* src = a.y;
     if (v == 1 && a.m) src = a.m;
     if (v == 2 && a.off) src = a.off;
@@ -271,23 +299,29 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
 }
 
 // Pipeline per row block i (cur = i & 1), ONE barrier per block:
-//   MFMA-only waves:  MFMA k-steps 0-7 of block i                              | barrier
-//   row waves:        MFMA k 0-3 of i; wait for their own LDS-DMA of block i+1;
-//                     row stage of block i+1 (w, w*z); MFMA k 4-7 of i         | barrier;
+//   MFMA-only waves ("issuers"): MFMA k 0..KA-1 of block i; wait for their own LDS-DMA of
+//                     block i+1 and publish it (LDS counter); MFMA k KA..7      | barrier;
 //                     LDS-DMA of block i+2 into the buffer block i occupied.
-// A wave's own LDS-DMA is complete at its vmcnt wait, so only the end-of-block barrier
-// orders the image / w buffers across waves.  The row waves carry the critical path (their
-// MFMAs + the row stage) and run at raised priority; the MFMA-only partner on the same SIMD
-// fills the gaps.
+//   row waves:        MFMA k 0..K1-1 of i; wait until every issuer published block i+1;
+//                     row stage of block i+1 (w, w*z); MFMA k K1..7 of i       | barrier
+// Only the end-of-block barrier orders the image and the w buffers across all waves.  The
+// DMA issue (a burst the memory queues throttle to ~5k cycles per block) sits on the issuers,
+// which have slack at the barrier; the row waves carry the critical path (their MFMAs + the
+// row stage) at raised priority.  Measured per-phase with tools/stamps.py (-DSGLM_STAMPS).
 template <int P16, int FAM, int LNK, int WV>
 __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv, int lane) {
   using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
   const bool do_gram = !(a.dbg & 2);
-  const int rw = wv - G::ROW0;
-  const bool row_wave = rw >= 0 && rw < G::NRW;
+  // roles are compile-time per wave (WV), so each wave's instantiation carries only its code
+  constexpr int rw = WV - G::ROW0;
+  constexpr bool row_wave = rw >= 0 && rw < G::NRW;
+  // DMA issuer index: the MFMA-only waves in order (or the only wave)
+  constexpr bool issuer = G::NA > 0 ? !row_wave : true;
+  constexpr int si = G::NA > 0 ? (WV < G::ROW0 ? WV : WV - G::NRW) : 0;
   constexpr int K1 = SGLM_K1;  // MFMA k-steps of block i before the row stage of block i+1
+  constexpr int KA = SGLM_KA;  // ... before an issuer publishes its landed part of block i+1
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
   d4 acc[G::ntiles(WV)];
@@ -295,9 +329,9 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   for (int k = 0; k < G::ntiles(WV); ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
 
-  if (row_wave && b0 < b1) {
-    stage_block<P16>(lds, 0, a, b0, rw, lane);
-    if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, rw, lane);
+  if (issuer && b0 < b1) {
+    stage_block<P16>(lds, 0, a, b0, si, lane);
+    if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, si, lane);
   }
   if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(1);
   // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
@@ -307,24 +341,50 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     const int cur = (int)((blk - b0) & 1);  // buffers of block blk; block blk+1 uses cur ^ 1
     const bool has_gram = blk >= b0 && do_gram;
     const bool has_next = blk + 1 < b1;
-    if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
-    if (row_wave && has_next) {
-      // this wave's part of block blk+1 landed (prologue: block b0+1 may still fly behind b0)
-      if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QRW + G::VRW>();
-      else wait_vmcnt<0>();
-      // ... and every row wave's part: the row waves count landed parts in LDS (each row
-      // needs all columns; the MFMA-only waves are not held up by this)
-      if constexpr (G::NRW > 1) {
-        if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const unsigned target = (unsigned)(G::NRW * (blk + 2 - b0));
-        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-          __builtin_amdgcn_s_sleep(1);
+    SGLM_STAMP(0);
+    if constexpr (G::NA > 0) {
+      if constexpr (!row_wave) {
+        // MFMA-only wave: after KA k-steps, publish that its part of block blk+1 has landed
+        if (has_gram) gram_steps<P16, WV, KA>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+        SGLM_STAMP(1);
+        if (has_next) {
+          wait_vmcnt<0>();
+          SGLM_STAMP(2);
+          if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        SGLM_STAMP(3);
+        SGLM_STAMP(4);
+        if (has_gram) gram_steps<P16, WV, RB / 4 - KA>(lds, cur & 1, cur & 1, lane, KA, acc, xz_lo, xz_hi);
+      } else {
+        // row wave: after K1 k-steps, wait until every issuer's part of block blk+1 landed
+        if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+        SGLM_STAMP(1);
+        SGLM_STAMP(2);
+        if (has_next) {
+          const unsigned target = (unsigned)(G::NA * (blk + 2 - b0));
+          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+            __builtin_amdgcn_s_sleep(1);
+          SGLM_STAMP(3);
+          if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+        }
+        SGLM_STAMP(4);
+        if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
       }
-      if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+    } else {
+      // single wave: it stages, waits and computes everything itself
+      if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+      if (has_next) {
+        if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
+        else wait_vmcnt<0>();
+        if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+      }
+      if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
     }
-    if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
+    SGLM_STAMP(5);
     lds_barrier();
-    if (row_wave && blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, rw, lane);
+    SGLM_STAMP(6);
+    if (issuer && blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
+    SGLM_STAMP(7);
   }
   if (row_wave) __builtin_amdgcn_s_setprio(0);
 

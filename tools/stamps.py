@@ -1,0 +1,30 @@
+"""Phase timeline of the fused pass (diagnostic build with -DSGLM_STAMPS, see kernels.hip):
+per wave of workgroup 0, the mean cycles of each phase over 16 steady-state row blocks.
+usage: SGLM_LIB=sparkglm_amd/lib_ab/stamps.so AN=20000000 AP=256 python tools/stamps.py"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sparkglm_amd import Engine, _lib  # noqa: E402
+
+n, p = int(os.environ.get("AN", "20000000")), int(os.environ.get("AP", "256"))
+e = Engine(0)
+e.synth(0, 0, n, p, 2)
+b = np.full(p, 0.01)
+e.irls_pass(b)
+e.irls_pass(b)
+lib = _lib.load()
+buf = (C.c_ulonglong * (8 * 16 * 8))()
+assert lib.sglm_debug_stamps(buf, 8 * 16 * 8) == 0
+t = np.array(buf, dtype=np.float64).reshape(8, 16, 8)
+names = ["gram k0-3", "dma wait", "flag spin", "row stage", "gram k4-7", "barrier", "dma issue"]
+t0 = t[:, :, 0].min()
+print("wave  " + "  ".join(f"{s:>10s}" for s in names) + "   block total")
+for w in range(8):
+    d = np.diff(t[w], axis=1)  # [16][7]
+    row = d.mean(axis=0)
+    tot = np.diff(t[w, :, 0]).mean()
+    print(f"{w:4d}  " + "  ".join(f"{v:10.0f}" for v in row) + f"   {tot:8.0f}")

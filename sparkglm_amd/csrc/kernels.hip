@@ -23,10 +23,10 @@
 #include "rowmath.hpp"
 
 #ifndef SGLM_K1
-#define SGLM_K1 6
+#define SGLM_K1 -1
 #endif
 #ifndef SGLM_KA
-#define SGLM_KA 2
+#define SGLM_KA -1
 #endif
 #ifndef SGLM_PRIO
 #define SGLM_PRIO 1
@@ -320,8 +320,10 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   // DMA issuer index: the MFMA-only waves in order (or the only wave)
   constexpr bool issuer = G::NA > 0 ? !row_wave : true;
   constexpr int si = G::NA > 0 ? (WV < G::ROW0 ? WV : WV - G::NRW) : 0;
-  constexpr int K1 = SGLM_K1;  // MFMA k-steps of block i before the row stage of block i+1
-  constexpr int KA = SGLM_KA;  // ... before an issuer publishes its landed part of block i+1
+  // MFMA k-steps of block i before the row stage of block i+1 (K1) and before an issuer
+  // publishes its landed part of block i+1 (KA); A/B-measured per variant (tools/ab.py)
+  constexpr int K1 = SGLM_K1 >= 0 ? SGLM_K1 : (P16 == 16 ? 7 : 6);
+  constexpr int KA = SGLM_KA >= 0 ? SGLM_KA : (P16 == 16 ? 0 : 2);
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
   d4 acc[G::ntiles(WV)];

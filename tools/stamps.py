@@ -20,7 +20,7 @@ lib = _lib.load()
 buf = (C.c_ulonglong * (8 * 16 * 8))()
 assert lib.sglm_debug_stamps(buf, 8 * 16 * 8) == 0
 t = np.array(buf, dtype=np.float64).reshape(8, 16, 8)
-names = ["gram k0-3", "dma wait", "flag spin", "row stage", "gram k4-7", "barrier", "dma issue"]
+names = ["gram 1st", "vmcnt", "flag", "row stage", "gram 2nd", "barrier", "dma issue"]
 t0 = t[:, :, 0].min()
 print("wave  " + "  ".join(f"{s:>10s}" for s in names) + "   block total")
 for w in range(8):

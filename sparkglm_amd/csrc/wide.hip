@@ -26,6 +26,10 @@
 #include "procx.hpp"
 #include "rowmath.hpp"
 
+#ifndef WIDE_SPREAD_DMA
+#define WIDE_SPREAD_DMA 1
+#endif
+
 namespace sglm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -238,6 +242,14 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
         if (s == 1) wstage<false, true, 2, 4>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
         if (s == 2) wstage<false, true, 4, 6>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
         if (s == 3) wstage<false, true, 6, 8>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+      });
+    } else if (WIDE_SPREAD_DMA) {  // issue block blk+1's DMA two octets per k-step, under the MFMAs
+      offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
+        if (!next) return;
+        if (s == 0) wstage<false, false, 0, 2>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 1) wstage<false, false, 2, 4>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 2) wstage<false, false, 4, 6>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 3) wstage<false, false, 6, 8>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
       });
     } else {
       if (next) wstage<false, false>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);

@@ -288,7 +288,7 @@ struct sglm_engine : public Backend {
       P16 = narrow_variant((int)p);
       stride = narrow_stride(P16);
       const int64_t want_grid = (int64_t)ncu * narrow_wg_per_cu();
-      const int64_t per_wg = narrow_rows_per_wg();
+      const int64_t per_wg = narrow_rows_per_wg(P16);
       const int64_t need = (nblocks * RB + per_wg - 1) / per_wg;
       grid = (int)std::max<int64_t>(1, std::min(need, want_grid));
     } else {

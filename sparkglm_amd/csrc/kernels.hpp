@@ -26,7 +26,7 @@ hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed,
 int narrow_variant(int p);      // column blocks of 16 (1..4)
 int narrow_stride(int P16);     // doubles per workgroup partial (reduce_partials_kernel layout)
 int narrow_wg_per_cu();
-int narrow_rows_per_wg();       // rows one workgroup streams per block step (waves x 16)
+int narrow_rows_per_wg(int P16); // rows one workgroup streams per block step (waves x rows per block)
 hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st);
 
 // wide path (wide.hip)

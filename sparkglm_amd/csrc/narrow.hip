@@ -34,6 +34,24 @@
 #include "kernels.hpp"
 #include "rowmath.hpp"
 
+#ifdef SGLM_STAMPS
+// Diagnostic build only (tools/stamps.py NARROW=1): per-phase s_memtime stamps of workgroup
+// 0's waves over 16 steady-state blocks.  [wave 8][block 16][event 8]
+__device__ unsigned long long sglm_nstamp_buf[8 * 16 * 8];
+#define NSTAMP(ev)                                                                                  \
+  do {                                                                                              \
+    if (blockIdx.x == 0 && blk >= b0 + 100 && blk < b0 + 116 && lane == 0)                          \
+      sglm_nstamp_buf[(wv * 16 + (int)(blk - b0 - 100)) * 8 + (ev)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+extern "C" int sglm_debug_nstamps(unsigned long long* out, long count) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_nstamp_buf), sizeof(unsigned long long) * count);
+}
+#else
+#define NSTAMP(ev) \
+  do {             \
+  } while (0)
+#endif
+
 namespace sglm {
 
 namespace {
@@ -41,7 +59,10 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int NWAVE = 8;   // waves per workgroup (two per SIMD), one workgroup per CU
+#ifndef SGLM_NPRIO
+#define SGLM_NPRIO 4
+#endif
+constexpr int NPRIO = SGLM_NPRIO;
 
 // Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
 // (LDS: 8 waves x 2 buffers).  Row swizzle f(c): 2((c >> 1) & 7) at NRB = 16 (the column
@@ -49,6 +70,10 @@ constexpr int NWAVE = 8;   // waves per workgroup (two per SIMD), one workgroup 
 template <int P16>
 struct NGeo {
   static_assert(P16 >= 1 && P16 <= 4, "narrow variants: p <= 64");
+  // 8 waves per workgroup (two per SIMD), one workgroup per CU.  (Measured: 12 or 16 waves on
+  // 16-row blocks at p <= 32 run 1.2-1.7x slower -- the family arithmetic's lane efficiency,
+  // not latency, bounds these variants.)
+  static constexpr int NW = 8;
   static constexpr int NRB = P16 <= 2 ? 32 : 16;     // rows per block
   static constexpr int LPR = 64 / NRB;               // row-stage lanes per row
   static constexpr int NC = 16 * P16;                // padded columns
@@ -65,7 +90,8 @@ struct NGeo {
   static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB]
   static constexpr int WAVE_LDS = OFF_W + 2 * NRB;   // doubles per wave
   static constexpr int PSZ = T * 256 + NC + 2;       // one wave partial (tiles | X'Wz | dev, sum w)
-  static constexpr int LDS = (NWAVE * WAVE_LDS > 4 * PSZ) ? NWAVE * WAVE_LDS : 4 * PSZ;
+  static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
+  static_assert(NW % 4 == 0, "whole waves per SIMD");
   static constexpr int STRIDE = T * 256 + NC + NS;   // global partial (reduce_partials_kernel layout)
   static_assert(LDS * 8 <= 160 * 1024, "LDS budget");
 };
@@ -113,7 +139,7 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
 }
 
 template <int P16, int FAM, int LNK>
-__global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) {
+__global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
   __shared__ double lds[G::LDS];
@@ -122,7 +148,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
   double* wl = lds + wv * G::WAVE_LDS;
 
   const int64_t nb = a.nblocks * (RB / NRB);  // NRB-row blocks (n_pad = nblocks * RB)
-  const int64_t gw = (int64_t)blockIdx.x * NWAVE + wv, nwt = (int64_t)gridDim.x * NWAVE;
+  const int64_t gw = (int64_t)blockIdx.x * G::NW + wv, nwt = (int64_t)gridDim.x * G::NW;
   const int64_t b0 = nb * gw / nwt, b1 = nb * (gw + 1) / nwt;
   const int ngrp_stored = ((a.p + 7) / 8 * 8) / G::CPI;  // X stores whole column octets
   const bool irls = a.mode == MODE_IRLS;
@@ -172,10 +198,19 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int buf = (int)((blk - b0) & 1);
+    // The two waves sharing a SIMD (wv, wv ^ 4) take turns at the higher issue priority every
+    // NPRIO blocks: the arbiter otherwise favours the older wave, the younger one falls ~35 %
+    // behind on its equal share and finishes alone with no partner to overlap.
+    if (NPRIO > 0) {
+      if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+    NSTAMP(0);
     // block blk landed; block blk+1 (and the previous block's eta store) may still fly
     if (blk + 1 >= b1) wait_vm<0>();
     else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
     else wait_vm<G::NOCT + 1>();
+    NSTAMP(1);
     const double* xs = wl + buf * G::BUF;
 
     // ---- row stage ----
@@ -211,6 +246,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
       wl[G::OFF_W + NRB + rl] = wz;
     }
 
+    NSTAMP(2);
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
     if (do_gram) {
 #pragma unroll
@@ -235,7 +271,9 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
     }
     // every LDS read of this buffer has returned before the DMA may overwrite it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    NSTAMP(3);
     if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+    NSTAMP(4);
   }
 
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
@@ -247,13 +285,15 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
     s_aux += __shfl_xor(s_aux, o);
   }
 
-  // ---- fixed-order tree over the 8 waves in LDS: ((w0+w4)+(w2+w6)) + ((w1+w5)+(w3+w7)) ----
+  // ---- fixed-order fold over the NW waves in LDS: while n > 1, waves [h, n) (h = ceil(n/2))
+  // hand their partials to waves [0, n - h) (NW = 8: ((w0+w4)+(w2+w6)) + ((w1+w5)+(w3+w7))) ----
   wait_vm<0>();
   __syncthreads();
 #pragma unroll 1
-  for (int half = NWAVE / 2; half >= 1; half >>= 1) {
-    if (wv >= half && wv < 2 * half) {
-      double* reg = lds + (wv - half) * G::PSZ;
+  for (int n = G::NW; n > 1;) {
+    const int h = (n + 1) / 2;
+    if (wv >= h && wv < n) {
+      double* reg = lds + (wv - h) * G::PSZ;
 #pragma unroll
       for (int t = 0; t < G::T; ++t)
 #pragma unroll
@@ -268,7 +308,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
       }
     }
     __syncthreads();
-    if (wv < half) {
+    if (wv < n - h) {
       const double* reg = lds + wv * G::PSZ;
 #pragma unroll
       for (int t = 0; t < G::T; ++t)
@@ -280,6 +320,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
       s_aux += reg[G::T * 256 + G::NC + 1];
     }
     __syncthreads();
+    n = h;
   }
   if (wv == 0) {
     double* out = a.partials + (int64_t)blockIdx.x * a.stride;
@@ -297,7 +338,7 @@ __global__ void __launch_bounds__(64 * NWAVE, 1) irls_narrow_kernel(PassArgs a) 
 
 template <int P16>
 hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st) {
-  const dim3 gr(grid), bl(64 * NWAVE);
+  const dim3 gr(grid), bl(64 * NGeo<P16>::NW);
   const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
@@ -322,7 +363,14 @@ hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st) {
 int narrow_variant(int p) { return (p + 15) / 16; }
 int narrow_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS; }
 int narrow_wg_per_cu() { return 1; }
-int narrow_rows_per_wg() { return 16 * NWAVE; }
+int narrow_rows_per_wg(int P16) {
+  switch (P16) {
+    case 1: return NGeo<1>::NRB * NGeo<1>::NW;
+    case 2: return NGeo<2>::NRB * NGeo<2>::NW;
+    case 3: return NGeo<3>::NRB * NGeo<3>::NW;
+    default: return NGeo<4>::NRB * NGeo<4>::NW;
+  }
+}
 
 hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st) {
   switch (P16) {

@@ -11,16 +11,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sparkglm_amd import Engine, _lib  # noqa: E402
 
 n, p = int(os.environ.get("AN", "20000000")), int(os.environ.get("AP", "256"))
+narrow = os.environ.get("NARROW") == "1"
+kind = int(os.environ.get("AK", "0"))
+fam, lnk = os.environ.get("AF", "binomial"), os.environ.get("AL", "logit")
 e = Engine(0)
-e.synth(0, 0, n, p, 2)
+e.synth(kind, 0, n, p, 2)
 b = np.full(p, 0.01)
-e.irls_pass(b)
-e.irls_pass(b)
+e.irls_pass(b, family=fam, link=lnk)
+e.irls_pass(b, family=fam, link=lnk)
 lib = _lib.load()
 buf = (C.c_ulonglong * (8 * 16 * 8))()
-assert lib.sglm_debug_stamps(buf, 8 * 16 * 8) == 0
+assert (lib.sglm_debug_nstamps if narrow else lib.sglm_debug_stamps)(buf, 8 * 16 * 8) == 0
 t = np.array(buf, dtype=np.float64).reshape(8, 16, 8)
-names = ["gram 1st", "vmcnt", "flag", "row stage", "gram 2nd", "barrier", "dma issue"]
+if narrow:
+    t = t[:, :, :5]
+names = (["vmcnt", "row stage", "gram", "dma issue"] if narrow else
+         ["gram 1st", "vmcnt", "flag", "row stage", "gram 2nd", "barrier", "dma issue"])
 t0 = t[:, :, 0].min()
 print("wave  " + "  ".join(f"{s:>10s}" for s in names) + "   block total")
 for w in range(8):

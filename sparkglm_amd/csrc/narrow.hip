@@ -70,9 +70,10 @@ constexpr int NPRIO = SGLM_NPRIO;
 template <int P16>
 struct NGeo {
   static_assert(P16 >= 1 && P16 <= 4, "narrow variants: p <= 64");
-  // 8 waves per workgroup (two per SIMD), one workgroup per CU.  (Measured: 12 or 16 waves on
-  // 16-row blocks at p <= 32 run 1.2-1.7x slower -- the family arithmetic's lane efficiency,
-  // not latency, bounds these variants.)
+  // 8 waves per workgroup (two per SIMD), one workgroup per CU.  (Measured at p <= 32: 12 or
+  // 16 waves on 16-row blocks run 1.2-1.7x slower -- the family arithmetic's lane efficiency,
+  // not latency, bounds these variants -- and 4 waves on 64-row blocks (all 64 lanes in the
+  // family arithmetic, no partner wave) 1.07-1.17x slower.)
   static constexpr int NW = 8;
   static constexpr int NRB = P16 <= 2 ? 32 : 16;     // rows per block
   static constexpr int LPR = 64 / NRB;               // row-stage lanes per row

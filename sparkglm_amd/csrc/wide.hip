@@ -300,54 +300,69 @@ __global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a
   }
 }
 
-// Row stage: thread per row, columns streamed in order with four partial sums.
+// Row stage: thread per row PAIR (16-byte loads of two adjacent rows of each column),
+// columns streamed in order with four partial sums per row.
 template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
   __shared__ double red[4][2];
-  const int64_t per = (a.n_pad + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = per * blockIdx.x, hi = (lo + per < a.n_pad) ? lo + per : a.n_pad;
+  const int64_t np2 = a.n_pad / 2;  // row pairs (n_pad is even)
+  const int64_t per = (np2 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = (lo + per < np2) ? lo + per : np2;
   double s_dev = 0.0, s_aux = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    double eta = 0.0;
+  for (int64_t i2 = lo + threadIdx.x; i2 < hi; i2 += blockDim.x) {
+    const int64_t i = 2 * i2;
+    double eta[2] = {0.0, 0.0};
     if (a.mode == MODE_IRLS) {
-      double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
+      double e[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
       if (a.proc.on) {  // procedural design: same partial-sum order as the resident image
-        int j = 0;
-        for (; j + 4 <= a.p; j += 4) {
-          e0 += proc_x(a.proc, i, j) * a.beta[j];
-          e1 += proc_x(a.proc, i, j + 1) * a.beta[j + 1];
-          e2 += proc_x(a.proc, i, j + 2) * a.beta[j + 2];
-          e3 += proc_x(a.proc, i, j + 3) * a.beta[j + 3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          int j = 0;
+          for (; j + 4 <= a.p; j += 4)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) e[r][q] += proc_x(a.proc, i + r, j + q) * a.beta[j + q];
+          for (; j < a.p; ++j) e[r][0] += proc_x(a.proc, i + r, j) * a.beta[j];
         }
-        for (; j < a.p; ++j) e0 += proc_x(a.proc, i, j) * a.beta[j];
-        eta = (e0 + e1) + (e2 + e3);
-      }
-      const double* xc = a.X + i;
-      int j = a.proc.on ? a.p : 0;
+      } else {
+        const double* xc = a.X + i;
+        int j = 0;
 #pragma unroll 2
-      for (; j + 4 <= a.p; j += 4) {
-        e0 += xc[(int64_t)j * a.ld] * a.beta[j];
-        e1 += xc[(int64_t)(j + 1) * a.ld] * a.beta[j + 1];
-        e2 += xc[(int64_t)(j + 2) * a.ld] * a.beta[j + 2];
-        e3 += xc[(int64_t)(j + 3) * a.ld] * a.beta[j + 3];
+        for (; j + 4 <= a.p; j += 4)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const double2 v = *(const double2*)(xc + (int64_t)(j + q) * a.ld);
+            const double b = a.beta[j + q];
+            e[0][q] += v.x * b;
+            e[1][q] += v.y * b;
+          }
+        for (; j < a.p; ++j) {
+          const double2 v = *(const double2*)(xc + (int64_t)j * a.ld);
+          e[0][0] += v.x * a.beta[j];
+          e[1][0] += v.y * a.beta[j];
+        }
       }
-      for (; j < a.p; ++j) e0 += xc[(int64_t)j * a.ld] * a.beta[j];
-      if (!a.proc.on) eta = (e0 + e1) + (e2 + e3);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) eta[r] = (e[r][0] + e[r][1]) + (e[r][2] + e[r][3]);
     }
-    double w = 0.0, wz = 0.0;
-    if (i < a.n) {
-      const double y = a.y[i];
-      const double m = a.m ? a.m[i] : 1.0;
-      const double off = a.off ? a.off[i] : 0.0;
-      const double pw = a.prior ? a.prior[i] : 1.0;
-      if (a.mode == MODE_IRLS) {
-        eta = eta + off;
-        if (a.eta_out) a.eta_out[i] = eta;
+    double w[2] = {0.0, 0.0}, wz[2] = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t row = i + r;
+      if (row < a.n) {
+        const double y = a.y[row];
+        const double m = a.m ? a.m[row] : 1.0;
+        const double off = a.off ? a.off[row] : 0.0;
+        const double pw = a.prior ? a.prior[row] : 1.0;
+        double et = eta[r];
+        if (a.mode == MODE_IRLS) {
+          et = et + off;
+          if (a.eta_out) a.eta_out[row] = et;
+        }
+        pass_row(FAM, LNK, a.mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w[r], wz[r], s_dev, s_aux);
       }
-      pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
     }
-    a.w[i] = w;
-    a.wz[i] = wz;
+    *(double2*)(a.w + i) = double2{w[0], w[1]};
+    *(double2*)(a.wz + i) = double2{wz[0], wz[1]};
   }
   for (int o = 1; o < 64; o <<= 1) {
     s_dev += __shfl_xor(s_dev, o);

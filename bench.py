@@ -164,13 +164,23 @@ def main() -> int:
         from sparkglm_amd.distributed import torch_allreduce
         eng.set_comm(torch_allreduce(), on_device=False)
     elif dist_on:
-        if args.comm == "rccl":
-            uid = [Engine.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            eng.set_comm_rccl(world, rank, uid[0])
-        else:
+        comm = args.comm
+        if comm == "rccl":  # the engine's own RCCL communicator (sglm_set_comm_rccl)
+            try:
+                uid = [Engine.rccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                eng.set_comm_rccl(world, rank, uid[0])
+            except Exception as exc:  # same RCCL, reached through torch's process group instead
+                log(f"[rank {rank}] engine RCCL communicator unavailable ({exc}); using torch's RCCL group")
+                comm = "torch"
+            ok = torch.tensor([1 if comm == "rccl" else 0], device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                comm = "torch"
+        if comm != "rccl":
             from sparkglm_amd.distributed import torch_allreduce
             eng.set_comm(torch_allreduce(), on_device=True)
+        args.comm = comm
     log(f"[rank {rank}] shard {n} x {p} ({args.workload}) generated in {gen_s:.2f} s")
 
     # time-to-converge: a full fit (data resident), reference semantics (tol 1e-6)
@@ -244,6 +254,7 @@ def main() -> int:
             "data": "synthetic (seeded counter-based generator, generated in HBM)",
             "config": {"workload": wl["label"], "bench_workload": args.workload,
                        "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}" + ("-shared-device-gloo" if shared else ""),
+                       "allreduce": "gloo" if shared else ("rccl-engine" if args.comm == "rccl" else "rccl-torch"),
                        "family": fam, "link": lnk, "tol": 1e-6,
                        "offset_prior": wl["kind"] == 2, "procedural_x": wl.get("procedural", False)},
             "time_to_converge_s": ttc,

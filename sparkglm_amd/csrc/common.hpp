@@ -47,7 +47,8 @@ struct PassArgs {
   double* partials;     // [grid][stride]
   int64_t stride;
   double* eta_out;      // optional [n]: eta of MODE_IRLS rows (for the final statistics)
-  int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math
+  int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math,
+                        // 32 no eta store
 };
 
 // ---- wide-design path (p > 16*MAX_P16): row kernel + panel-pair Gram kernel ----

@@ -411,7 +411,7 @@ struct sglm_engine : public Backend {
     a.ybar = ybar;
     a.partials = dpart;
     a.stride = stride;
-    a.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
+    a.eta_out = (mode == MODE_IRLS && !(dbg & 32)) ? deta : nullptr;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (wide) {

@@ -24,6 +24,46 @@ __device__ __forceinline__ double norm_pdf(double x) {
   return exp(-d * d / 2.0 - (log(sqrt(2.0 * M_PI)) + log(1.0)));
 }
 
+// Reciprocal of a positive normal x: v_rcp_f64 plus two Newton steps (quadratic convergence
+// from the hardware estimate), ~1 ulp -- the fast paths below use it in place of the IEEE
+// division sequence (div_scale / div_fmas / div_fixup), which they never need: their operands
+// are bounded away from 0, denormals and infinity by the fast-path range checks.
+__device__ __forceinline__ double rcp_pos(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+
+// Natural log of a positive finite x (normal or denormal), ~2 ulp: x = m 2^k with
+// m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m - 1)/(m + 1), |s| <= 0.1716, as
+// 2s (1 + s^2/3 + ... + s^18/19) (truncation < 3e-17 relative).  The row fast paths use it
+// for the deviance terms instead of libm's double-double log / log1p (about 3x fewer
+// instructions); the per-row values differ from libm's by a few ulp, far inside the 1e-9
+// parity tolerance on the summed deviance.
+__device__ __forceinline__ double log_pos(double x) {
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  int k = __builtin_amdgcn_frexp_exp(x);
+  if (m < 0.70710678118654752440) {
+    m = m + m;
+    k -= 1;
+  }
+  const double f = m - 1.0;
+  const double s = f * rcp_pos(m + 1.0);
+  const double z = s * s;
+  double q = 1.0 / 19.0;
+  q = fma(q, z, 1.0 / 17.0);
+  q = fma(q, z, 1.0 / 15.0);
+  q = fma(q, z, 1.0 / 13.0);
+  q = fma(q, z, 1.0 / 11.0);
+  q = fma(q, z, 1.0 / 9.0);
+  q = fma(q, z, 1.0 / 7.0);
+  q = fma(q, z, 1.0 / 5.0);
+  q = fma(q, z, 1.0 / 3.0);
+  const double lm = fma(2.0 * s, z * q, 2.0 * s);
+  const double kd = (double)k;
+  return fma(kd, 6.93147180559945286227e-01, fma(kd, 2.31904681384629955842e-17, lm));
+}
+
 __device__ __forceinline__ double link_fn(int fam, int lnk, double mu, double m) {
   if (fam == FAM_BINOMIAL) {
     if (lnk == LNK_LOGIT) return log(mu / (m + (-1.0 * mu)));
@@ -107,16 +147,19 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
     //   dev row = y log(1/mu) + (1-y) log(1/(1-mu)) = log1p(e) + (1-y) eta
     // Inside |eta| < 8 both forms agree to ~1e-13 relative per row (1 - mu >= 3e-4, no
     // cancellation); outside it, and for m != 1, the reference operation order below applies.
+    // u = 1 + e lies in (1, 2982): t = 1/u by rcp_pos, and log1p(e) = log(u) + (e - (u - 1))/u
+    // (the rounding of u corrected to first order, as libm's log1p does).
     const double e = exp(-eta);
-    const double t = 1.0 / (1.0 + e);
+    const double u = 1.0 + e;
+    const double t = rcp_pos(u);
     const double v = e * t * t;
     w = pw * v;
     wz = pw * (v * (eta - off) + (y - t));
-    s_dev += pw * (log1p(e) + (1.0 - y) * eta);
+    s_dev += pw * (fma(e - (u - 1.0), t, log_pos(u)) + (1.0 - y) * eta);
     s_aux += pw;
     return;
   }
-  if (fam == FAM_POISSON && mode == MODE_IRLS && fabs(eta) < 700.0 && y >= 0.0) {
+  if (fam == FAM_POISSON && mode == MODE_IRLS && fabs(eta) < 700.0 && y >= 0.0 && y < 1e300) {
     // Poisson / log (R's poisson()): mu = exp(eta), g' = 1/mu, V = mu, so
     //   w = 1/(V g'^2) = mu,  w*z = mu (eta - off) + (y - mu),
     //   dev row = y log(y/mu) - (y - mu) with log(y/mu) = log(y) - eta
@@ -125,21 +168,22 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
     const double mu = exp(eta);
     w = pw * mu;
     wz = pw * (mu * (eta - off) + (y - mu));
-    s_dev += pw * ((y > 0.0 ? y * (log(y) - eta) : 0.0) - (y - mu));
+    s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
     s_aux += pw;
     return;
   }
-  if (fam == FAM_GAMMA && mode == MODE_IRLS && eta > 0.0 && eta < 1e150 && y > 0.0) {
+  if (fam == FAM_GAMMA && mode == MODE_IRLS && eta > 1e-150 && eta < 1e150 && y > 1e-150 && y < 1e150) {
     // Gamma / inverse (R's Gamma()): mu = 1/eta, g' = -1/mu^2, V = mu^2, so
     //   w = mu^2,  w*z = mu^2 (eta - off) - (y - mu),
     //   dev row = -(log(y/mu) - (y - mu)/mu) = -(log(y eta) - (y eta - 1))
-    // -- one division and one log instead of four divisions and a log.
-    const double mu = 1.0 / eta;
+    // -- one reciprocal and one log instead of four divisions and a log (the range checks keep
+    // eta, y and y eta normal and finite for rcp_pos / log_pos).
+    const double mu = rcp_pos(eta);
     const double mu2 = mu * mu;
     const double ye = y * eta;
     w = pw * mu2;
     wz = pw * (mu2 * (eta - off) - (y - mu));
-    s_dev += pw * (-(log(ye) - (ye - 1.0)));
+    s_dev += pw * (-(log_pos(ye) - (ye - 1.0)));
     s_aux += pw;
     return;
   }

@@ -8,7 +8,7 @@ one IRLS iteration: the fused pass over every resident row (eta, mu, w, z, devia
 the X'WX / X'Wz Gramian on fp64 MFMA) + the all-reduce over ranks + the p x p solve.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-                  [--workload logit256|poisson64|gamma2048|logit512|logit512r|logit1b]
+                  [--workload logit256|poisson64|gamma2048|logit512|logit512r|logit1b|lm20]
                   [--rows R] [--p P]
 
 N > 1 is launched by torch.distributed.run (one process per GPU); each rank holds its
@@ -42,6 +42,10 @@ def log(*a):
 # are measured with --workload and recorded under profiles/ (rows per GPU = the config's global
 # rows / 8 where the config is quoted on 8 GPUs, or the largest resident shard, as labelled).
 WORKLOADS = {
+    "lm20": dict(cfg=0, kind=1, family="gaussian", link="identity", p=20, rows=1_000_000, seed=1, lm=True,
+                 cpu_rows=1_000_000,
+                 label="gaussian lm (least squares, LM.fit) on a synthetic 1M x 20 dense design (BASELINE "
+                       "configs[0]); a step is one LM fit: Gram pass + solve + residual pass"),
     "logit256": dict(cfg=1, kind=0, family="binomial", link="logit", p=256, rows=100_000_000, seed=2,
                      cpu_rows=2_000_000,
                      label="binomial/logit glm, dense fp64 design, IRLS (BASELINE configs[1])"),
@@ -76,6 +80,17 @@ def cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
     from sparkglm_amd import synth
 
     X, y, off, prior = synth.generate(wl["kind"], 0, rows, p, wl["seed"])
+    if wl.get("lm"):
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            pyoracle.fit_lm(X, y, npart=threads, nthreads=threads)
+        dt = (time.perf_counter() - t0) / reps
+        return {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"CPU restatement of LM.fit / fitMultiple (oracle/sglm_oracle.c, -O3 AVX2, OpenMP), "
+                          f"{rows} x {p} rows of the same generator, {threads} partitions/threads, mean of {reps} "
+                          f"fits ({dt * 1e3:.2f} ms each, not the JVM)",
+                "time_to_converge_s": dt, "iters": 1}
     t0 = time.perf_counter()
     fit = pyoracle.fit_glm(X, y, wl["family"], wl["link"], offset=off, prior=prior, npart=threads,
                            nthreads=threads)
@@ -183,6 +198,9 @@ def main() -> int:
         args.comm = comm
     log(f"[rank {rank}] shard {n} x {p} ({args.workload}) generated in {gen_s:.2f} s")
 
+    if wl.get("lm"):
+        return run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier)
+
     # time-to-converge: a full fit (data resident), reference semantics (tol 1e-6)
     barrier()
     t0 = time.perf_counter()
@@ -266,6 +284,62 @@ def main() -> int:
                                       "reduce": st["reduce_kernel_ms"] / passes,
                                       "solve": st["solve_ms"] / args.steps,
                                       "comm": st["comm_ms"] / args.steps},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+    return 0
+
+
+def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
+    """BASELINE configs[0]: LM.fit (LM.scala:241-274) on the resident shard.  A step is one whole
+    fit -- the Gram pass (narrow kernel, LM Gram mode), the all-reduce, the solve and the
+    residual pass (rowPartitionedSSE, LM.scala:160-188) -- so rows/s = rows fitted per second."""
+    import torch
+    import torch.distributed as dist
+    fit = eng.fit_lm()
+    for _ in range(max(args.warmup, 0)):
+        fit = eng.fit_lm()
+    eng.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fit = eng.fit_lm()
+    barrier()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    if dist_on:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if shared else "cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    if rank == 0:
+        passes = max(st["passes"], 1)
+        kern_ms = st["pass_kernel_ms"] / passes
+        bytes_pass = n * (8 * p + 8)  # X row + y, read once by the Gram pass (SURVEY 8d)
+        gbs = bytes_pass / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC, "value": n * world * args.steps / dt, "unit": "rows/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded counter-based generator, generated in HBM)",
+            "config": {"workload": wl["label"], "bench_workload": args.workload, "rows_per_gpu": n, "p": p,
+                       "global_rows": n * world, "parallelism": f"rows{world}", "family": "gaussian (LM)",
+                       "link": "identity"},
+            "time_to_converge_s": dt / args.steps, "iters_to_converge": 1,
+            "r2": fit.r2, "sse": fit.sse,
+            "roofline": {"bound": "hbm", "kernel": f"irls_narrow_kernel<{(p + 15) // 16},gaussian,identity> (LM Gram)",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "traffic": None, "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass,
+                         "note": "1M x 20 = 168 MB per pass: launch- and latency-bound, not a bandwidth test"},
+            "breakdown_ms_per_step": {"gram_pass_kernel": kern_ms, "reduce": st["reduce_kernel_ms"] / args.steps,
+                                      "solve": st["solve_ms"] / args.steps, "comm": st["comm_ms"] / args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)

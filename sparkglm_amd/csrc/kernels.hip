@@ -483,8 +483,19 @@ __global__ void reduce_partials_kernel(const double* __restrict__ part, int64_t 
     } else {
       src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
     }
+    // the same left-to-right order over the partials, with 32 loads in flight per thread (a
+    // dependent load-add chain over 256 partials is ~60 us of load latency)
+    const double* q = part + src;
     double s = 0.0;
-    for (int g = 0; g < nparts; ++g) s += part[(int64_t)g * stride + src];
+    int g = 0;
+    for (; g + 32 <= nparts; g += 32) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
+    for (; g < nparts; ++g) s += q[(int64_t)g * stride];
     out[e] = s;
   }
 }

@@ -241,7 +241,8 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if (a.dbg & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
-        else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
+        else
+          pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2);
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;

@@ -5,8 +5,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for wl in ${WLS:-logit256 poisson64 logit512 logit512r gamma2048 logit1b}; do
+for wl in ${WLS:-logit256 poisson64 logit512 logit512r gamma2048 logit1b lm20}; do
   steps=10; warm=2
+  [[ $wl == lm20 ]] && { steps=50; warm=5; }
   [[ $wl == gamma2048 || $wl == logit512 ]] && { steps=3; warm=1; }
   [[ $wl == logit1b ]] && { steps=5; warm=1; }
   timeout -k 10 400 python bench.py --workload $wl --steps $steps --warmup $warm > gpurun_out/bench_$wl.json 2> gpurun_out/bench_$wl.err

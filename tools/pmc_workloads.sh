@@ -7,8 +7,13 @@ run_wl() {  # name PN PP PKIND PF PL
   export PN=$2 PP=$3 PKIND=$4 PF=$5 PL=$6 PK=2
   bash tools/pmc_counters.sh "$name" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" || exit 1
 }
-run_wl poisson64 50000000 64 2 poisson log
-run_wl logit256 20000000 256 0 binomial logit
-run_wl logit512 8000000 512 0 binomial logit
-run_wl gamma2048 2000000 2048 3 gamma inverse
+for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
+  case $wl in
+    poisson64) run_wl poisson64 50000000 64 2 poisson log ;;
+    logit256) run_wl logit256 20000000 256 0 binomial logit ;;
+    logit512) run_wl logit512 8000000 512 0 binomial logit ;;
+    gamma2048) run_wl gamma2048 2000000 2048 3 gamma inverse ;;
+    logit32) run_wl logit32 100000000 32 0 binomial logit ;;   # logit1b's per-row pattern
+  esac
+done
 exit 0

@@ -78,7 +78,11 @@ struct NGeo {
   static constexpr int NRB = P16 <= 2 ? 32 : 16;     // rows per block
   static constexpr int LPR = 64 / NRB;               // row-stage lanes per row
   static constexpr int NC = 16 * P16;                // padded columns
-  static constexpr int T = P16 * (P16 + 1) / 2;      // lower-triangular tiles
+  // Lower-triangular 16x16 tiles.  (Measured and not kept: at P16 = 2 the two diagonal tiles
+  // as 4x4 blocks on v_mfma_f64_4x4x4f64 -- full rate on gfx950, tools/mfma44_*.hip -- with
+  // the off-diagonal tile on 16x16x4: 5 x 16 instead of 2 x 64 MFMA cycles per k-step, but the
+  // rotated operands' LDS reads and scaling made the compute-only pass 2-3 % slower.)
+  static constexpr int T = P16 * (P16 + 1) / 2;
   static constexpr int CPI = 128 / NRB;              // columns per DMA wave-instruction (1 KiB)
   static constexpr int NOCT = NC / CPI;              // DMA wave-instructions for X per block
   static constexpr int SPER = NRB == 16 ? 2 : 16 / CPI;  // period of the swizzle over column groups

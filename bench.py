@@ -129,6 +129,8 @@ def main() -> int:
     ap.add_argument("--cpu-rows", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the 1B x 32 strong-scaling point measured after the default workload")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
 
@@ -175,27 +177,7 @@ def main() -> int:
     t0 = time.perf_counter()
     eng.synth(wl["kind"], row0, n, p, seed, procedural=wl.get("procedural", False))  # this rank's shard
     gen_s = time.perf_counter() - t0
-    if shared:
-        from sparkglm_amd.distributed import torch_allreduce
-        eng.set_comm(torch_allreduce(), on_device=False)
-    elif dist_on:
-        comm = args.comm
-        if comm == "rccl":  # the engine's own RCCL communicator (sglm_set_comm_rccl)
-            try:
-                uid = [Engine.rccl_unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(uid, src=0)
-                eng.set_comm_rccl(world, rank, uid[0])
-            except Exception as exc:  # same RCCL, reached through torch's process group instead
-                log(f"[rank {rank}] engine RCCL communicator unavailable ({exc}); using torch's RCCL group")
-                comm = "torch"
-            ok = torch.tensor([1 if comm == "rccl" else 0], device="cuda")
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if int(ok.item()) == 0:
-                comm = "torch"
-        if comm != "rccl":
-            from sparkglm_amd.distributed import torch_allreduce
-            eng.set_comm(torch_allreduce(), on_device=True)
-        args.comm = comm
+    attach_comm(eng, args, world, rank, dist_on, shared)
     log(f"[rank {rank}] shard {n} x {p} ({args.workload}) generated in {gen_s:.2f} s")
 
     if wl.get("lm"):
@@ -216,7 +198,7 @@ def main() -> int:
     eng.reset_stats()
     barrier()
     t0 = time.perf_counter()
-    beta, dev = eng.irls_iterations(beta, args.steps, fam, lnk)
+    beta, _ = eng.irls_iterations(beta, args.steps, fam, lnk)
     barrier()
     dt = time.perf_counter() - t0
     st = eng.stats()
@@ -290,12 +272,99 @@ def main() -> int:
             out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
         else:
             out["cpu_baseline"] = None
+    eng.close()
+    if args.workload == "logit256" and not args.no_strong:
+        try:  # the north-star 1B-row strong-scaling point, beside the headline (own shard, freed after)
+            strong_1b_res = strong_1b(args, dev, world, rank, dist_on, shared, barrier)
+        except Exception as exc:  # never lose the headline line to the secondary measurement
+            log(f"[rank {rank}] strong-scaling 1B x 32 point failed: {exc}")
+            strong_1b_res = None
+        if rank == 0:
+            out["strong_scaling_1b_logit"] = strong_1b_res
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
-    eng.close()
     return 0
+
+
+def attach_comm(eng, args, world: int, rank: int, dist_on: bool, shared: bool) -> None:
+    """The engine's per-iteration all-reduce: its own RCCL communicator (sglm_set_comm_rccl),
+    else torch's RCCL group, or gloo over host buffers when ranks share a device."""
+    import torch
+    import torch.distributed as dist
+    from sparkglm_amd import Engine
+    if shared:
+        from sparkglm_amd.distributed import torch_allreduce
+        eng.set_comm(torch_allreduce(), on_device=False)
+    elif dist_on:
+        comm = args.comm
+        if comm == "rccl":  # the engine's own RCCL communicator (sglm_set_comm_rccl)
+            try:
+                uid = [Engine.rccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                eng.set_comm_rccl(world, rank, uid[0])
+            except Exception as exc:  # same RCCL, reached through torch's process group instead
+                log(f"[rank {rank}] engine RCCL communicator unavailable ({exc}); using torch's RCCL group")
+                comm = "torch"
+            ok = torch.tensor([1 if comm == "rccl" else 0], device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                comm = "torch"
+        if comm != "rccl":
+            from sparkglm_amd.distributed import torch_allreduce
+            eng.set_comm(torch_allreduce(), on_device=True)
+        args.comm = comm
+
+
+def strong_1b(args, dev: int, world: int, rank: int, dist_on: bool, shared: bool, barrier) -> dict:
+    """North-star strong-scaling point measured beside the headline: the 1B x 32 logistic GLM
+    (the logit1b workload) row-sharded over the N ranks of this run -- time to converge
+    (data resident) and the mean IRLS iteration time, max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from sparkglm_amd import Engine
+    from sparkglm_amd.distributed import shard_range
+    wl = WORKLOADS["logit1b"]
+    lo, hi = shard_range(wl["strong_rows"], world, rank)
+    eng = Engine(dev)
+    try:
+        ok = 1
+        try:
+            eng.synth(wl["kind"], lo, hi - lo, wl["p"], wl["seed"])
+        except Exception as exc:
+            log(f"[rank {rank}] 1B x 32 shard not generated: {exc}")
+            ok = 0
+        if dist_on:  # every rank takes the same branch before any collective of the fit
+            f = torch.tensor([ok], device="cpu" if shared else "cuda")
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = int(f.item())
+        if not ok:
+            raise RuntimeError("1B x 32 shard not generated on every rank")
+        attach_comm(eng, args, world, rank, dist_on, shared)
+        barrier()
+        t0 = time.perf_counter()
+        fit = eng.fit_glm(wl["family"], wl["link"], tol=1e-6)
+        barrier()
+        ttc = time.perf_counter() - t0
+        beta = np.array(fit.coefs, dtype=np.float64)
+        beta, _ = eng.irls_iterations(beta, 1, wl["family"], wl["link"])
+        k = 5
+        barrier()
+        t0 = time.perf_counter()
+        eng.irls_iterations(beta, k, wl["family"], wl["link"])
+        barrier()
+        it_s = (time.perf_counter() - t0) / k
+    finally:
+        eng.close()
+    if dist_on:
+        tt = torch.tensor([ttc, it_s], dtype=torch.float64, device="cpu" if shared else "cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ttc, it_s = float(tt[0]), float(tt[1])
+    return {"workload": "logit1b: " + wl["label"], "global_rows": wl["strong_rows"], "p": wl["p"],
+            "n_gpus": world, "scaling": "strong", "time_to_converge_s": ttc, "iters_to_converge": fit.iter,
+            "deviance": fit.deviance, "ms_per_iter": it_s * 1e3, "rows_per_s_per_iter": wl["strong_rows"] / it_s}
 
 
 def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:

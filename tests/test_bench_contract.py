@@ -37,3 +37,17 @@ def test_pmc_traffic_lookup():
     assert t is not None and 2000 * 1000 < t < 2200 * 1000
     assert bench.pmc_traffic(512, 10, "binomial", procedural=True) < bench.pmc_traffic(512, 10, "binomial")
     assert bench.pmc_traffic(333, 10, "binomial") is None
+
+
+def test_every_baseline_config_has_a_workload():
+    cfgs = json.load(open(os.path.join(ROOT, "BASELINE.json")))["configs"]
+    assert {wl["cfg"] for wl in bench.WORKLOADS.values()} == set(range(len(cfgs)))
+    assert bench.WORKLOADS["lm20"]["cfg"] == 0 and bench.WORKLOADS["lm20"].get("lm")
+
+
+def test_strong_scaling_point_and_p32_traffic():
+    # the default run appends the north-star 1B x 32 strong-scaling point (bench.strong_1b),
+    # whose per-row PMC traffic the logit1b roofline uses
+    assert callable(bench.strong_1b) and callable(bench.attach_comm)
+    t = bench.pmc_traffic(32, 1000, "binomial")
+    assert t is not None and 264 * 1000 <= t < 280 * 1000

@@ -531,7 +531,9 @@ struct sglm_engine : public Backend {
     a.mu0 = mu0;
     a.ybar = ybar;
     a.partials = dpart;
-    const int nb = 1024;
+    // one wave per SIMD leaves the per-row chain latency-bound on large shards; small ones
+    // (LM 1M x 20) keep 1024 partials for the host-side sum
+    const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
     HIPCHK(launch_stats(a, nb, st));
     std::vector<double> h((size_t)nb * NS);
     HIPCHK(hipMemcpyAsync(h.data(), dpart, sizeof(double) * h.size(), hipMemcpyDeviceToHost, st));

@@ -531,6 +531,9 @@ __global__ void ysum_kernel(const double* __restrict__ y, int64_t n, double* __r
 
 // Final-statistics pass over the resident vectors and the last pass's eta: one partial
 // of NS scalars per block, summed in a fixed order on the host side reduction.
+// One instantiation per family/link (as the pass kernels): an all-families kernel carried every
+// family's libm code (lgamma, erfinv, ...) at 438 VGPRs, one wave per SIMD, latency-bound.
+template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   __shared__ double red[4][NS];
   RowAcc acc;
@@ -542,7 +545,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
     const double m = a.m ? a.m[i] : 1.0;
     const double pw = a.prior ? a.prior[i] : 1.0;
     const double eta = a.eta ? a.eta[i] : 0.0;
-    stats_row(a.family, a.link, a.mode, eta, a.y[i], m, pw, a.mu0, a.ybar, a.m != nullptr, acc);
+    stats_row(FAM, LNK, a.mode, eta, a.y[i], m, pw, a.mu0, a.ybar, a.m != nullptr, acc);
   }
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -664,7 +667,21 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(256), 0, st, a);
+  const dim3 gr(grid), bl(256);
+  if (a.mode == MODE_LM_RESID || (a.family == FAM_GAUSSIAN && a.link == LNK_IDENTITY))
+    hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY>), gr, bl, 0, st, a);
+  else if (a.family == FAM_BINOMIAL && a.link == LNK_LOGIT)
+    hipLaunchKernelGGL((stats_kernel<FAM_BINOMIAL, LNK_LOGIT>), gr, bl, 0, st, a);
+  else if (a.family == FAM_BINOMIAL && a.link == LNK_PROBIT)
+    hipLaunchKernelGGL((stats_kernel<FAM_BINOMIAL, LNK_PROBIT>), gr, bl, 0, st, a);
+  else if (a.family == FAM_BINOMIAL && a.link == LNK_CLOGLOG)
+    hipLaunchKernelGGL((stats_kernel<FAM_BINOMIAL, LNK_CLOGLOG>), gr, bl, 0, st, a);
+  else if (a.family == FAM_POISSON && a.link == LNK_LOG)
+    hipLaunchKernelGGL((stats_kernel<FAM_POISSON, LNK_LOG>), gr, bl, 0, st, a);
+  else if (a.family == FAM_GAMMA && a.link == LNK_INVERSE)
+    hipLaunchKernelGGL((stats_kernel<FAM_GAMMA, LNK_INVERSE>), gr, bl, 0, st, a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

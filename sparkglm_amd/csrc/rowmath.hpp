@@ -263,19 +263,14 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
   s_aux += pw;
 }
 
-// Final statistics of one row at the converged mu: pearsonCalc (GLM.scala:90-101),
-// llBinomial (GLM.scala:132-143) and the extension families' loglik ingredients; LM
-// mode: SSE / SSR / SST terms of rowPartitionedSSE (LM.scala:172-175) with eta = X*coefs.
-__device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta, double y, double m, double pw,
-                                          double mu0, double ybar, bool has_m, RowAcc& acc) {
-  if (mode == MODE_LM_RESID) {
-    const double e = y - eta, t = eta + (-1.0 * ybar), b = y + (-1.0 * ybar);
-    acc.s[S_DEV] += e * e;
-    acc.s[S_PEARSON] += t * t;
-    acc.s[S_LL] += b * b;
-    acc.s[S_SUMW] += 1.0;
-    return;
-  }
+// The reference operation order of the final statistics (pearsonCalc GLM.scala:90-101,
+// llBinomial :132-143, devBinomial :162-170, the R families' loglik ingredients), out of line
+// like pass_row_ref: rows the inline fast path of stats_row does not take.
+__device__ __noinline__ RowAcc stats_row_ref(int fam, int lnk, int mode, double eta, double y, double m, double pw,
+                                             double mu0, bool has_m) {
+  RowAcc acc;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc.s[k] = 0.0;
   double mu;
   if (mode == MODE_IRLS) {
     mu = unlink_fn(fam, lnk, eta, m);
@@ -310,6 +305,43 @@ __device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta
     acc.s[S_AUX0] += pw * (y / mu);
     acc.s[S_AUX1] += pw * log(mu);
   }
+  return acc;
+}
+
+// Final statistics of one row at the converged mu: pearsonCalc (GLM.scala:90-101),
+// llBinomial (GLM.scala:132-143) and the extension families' loglik ingredients; LM
+// mode: SSE / SSR / SST terms of rowPartitionedSSE (LM.scala:172-175) with eta = X*coefs.
+__device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta, double y, double m, double pw,
+                                          double mu0, double ybar, bool has_m, RowAcc& acc) {
+  if (mode == MODE_LM_RESID) {
+    const double e = y - eta, t = eta + (-1.0 * ybar), b = y + (-1.0 * ybar);
+    acc.s[S_DEV] += e * e;
+    acc.s[S_PEARSON] += t * t;
+    acc.s[S_LL] += b * b;
+    acc.s[S_SUMW] += 1.0;
+    return;
+  }
+  if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT && mode == MODE_IRLS && !has_m && fabs(eta) < 8.0 && y >= 0.0 &&
+      y <= 1.0) {
+    // Logit, m = 1, the pass's fast-path forms (pass_row): mu = t = 1/(1+e), e = exp(-eta),
+    // V = mu(1 - mu) = e t^2, unit deviance log1p(e) + (1-y) eta, and Breeze's
+    // Binomial(1, mu).logProbabilityOf(k) = k log mu + (1-k) log(1-mu) with log mu = -log1p(e),
+    // log(1-mu) = -eta - log1p(e); |eta| < 8 keeps mu off 0 and 1 (no special cases, k in {0, 1}).
+    const double e = exp_small(-eta);
+    const double u = 1.0 + e;
+    const double t = rcp_pos(u);
+    const double L = fma(e - (u - 1.0), t, log_pos(u));
+    const double v = e * t * t;
+    const double r = y - t;
+    acc.s[S_DEV] += pw * (L + (1.0 - y) * eta);
+    acc.s[S_PEARSON] += pw * (r * r) * rcp_pos(v);
+    acc.s[S_SUMW] += pw;
+    acc.s[S_LL] += pw * ((int)y == 1 ? -L : -L - eta);
+    return;
+  }
+  const RowAcc r = stats_row_ref(fam, lnk, mode, eta, y, m, pw, mu0, has_m);
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc.s[k] += r.s[k];
 }
 
 }  // namespace sglm

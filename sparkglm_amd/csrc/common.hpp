@@ -29,6 +29,14 @@ inline int64_t tri_count(int64_t p) { return p * (p + 1) / 2; }
 inline int64_t packed_len(int64_t p) { return tri_count(p) + p + NS; }
 
 // Arguments of one fused pass launch.
+// Profiling ablations (SGLM_DEBUG_ABLATE, tools/ablate.py) exist only in the ablation build
+// (make ablate: -DSGLM_ABLATE=1, sparkglm_amd/lib_ablate/); the product kernels compile them
+// out so their main loops carry no debug branches.
+#ifndef SGLM_ABLATE
+#define SGLM_ABLATE 0
+#endif
+#define SGLM_DBG(a) (SGLM_ABLATE ? (a).dbg : 0)
+
 struct PassArgs {
   const double* X;      // col-major, leading dimension ld, 4*nq columns (zero past p)
   int64_t ld;

@@ -768,7 +768,9 @@ int sglm_create(int device, sglm_engine** out) {
   hipDeviceProp_t prop;
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e, "hipGetDeviceProperties");
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+#if SGLM_ABLATE  // ablation build only (make ablate)
   if (const char* ab = std::getenv("SGLM_DEBUG_ABLATE")) h->dbg = std::atoi(ab);
+#endif
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   *out = h;

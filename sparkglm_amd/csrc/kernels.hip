@@ -225,7 +225,7 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
   const int rl = lane % G::RW, g = lane / G::RW;
   const int r = G::RW * rw + rl;
   double eta = 0.0;
-  if (a.mode == MODE_IRLS && !(a.dbg & 8)) {
+  if (a.mode == MODE_IRLS && !(SGLM_DBG(a) & 8)) {
     // four independent partial sums per lane shorten the dependent FMA chain
     double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -253,7 +253,7 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
         eta = eta + off;
         if (a.eta_out) a.eta_out[row] = eta;
       }
-      if (a.dbg & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+      if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
     }
     lds[G::OFF_W + wb * 2 * RB + r] = w;
@@ -313,7 +313,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
-  const bool do_gram = !(a.dbg & 2);
+  const bool do_gram = !(SGLM_DBG(a) & 2);
   // roles are compile-time per wave (WV), so each wave's instantiation carries only its code
   constexpr int rw = WV - G::ROW0;
   constexpr bool row_wave = rw >= 0 && rw < G::NRW;
@@ -367,7 +367,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
           while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
             __builtin_amdgcn_s_sleep(1);
           SGLM_STAMP(3);
-          if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+          if (!(SGLM_DBG(a) & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
         }
         SGLM_STAMP(4);
         if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
@@ -378,14 +378,14 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
       if (has_next) {
         if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
         else wait_vmcnt<0>();
-        if (!(a.dbg & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+        if (!(SGLM_DBG(a) & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
       }
       if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
     }
     SGLM_STAMP(5);
     lds_barrier();
     SGLM_STAMP(6);
-    if (issuer && blk >= b0 && blk + 2 < b1 && !(a.dbg & 4)) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
+    if (issuer && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
     SGLM_STAMP(7);
   }
   if (row_wave) __builtin_amdgcn_s_setprio(0);

@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 
   const int cl = lane & 15, rq = lane >> 4;
   const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
-  const bool do_rows = !(a.dbg & 1), do_gram = !(a.dbg & 2), do_dma = !(a.dbg & 4);
+  const bool do_rows = !(SGLM_DBG(a) & 1), do_gram = !(SGLM_DBG(a) & 2), do_dma = !(SGLM_DBG(a) & 4);
 
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
   if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 
     // ---- row stage ----
     double eta = 0.0;
-    if (irls && !(a.dbg & 8)) {
+    if (irls && !(SGLM_DBG(a) & 8)) {
       double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int u = 0; u < CPL; ++u) {
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double m = a.m ? vv[NRB + rl] : 1.0;
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
-        if (a.dbg & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+        if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
         else
           pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2);
       }

@@ -225,7 +225,7 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   d4 acc[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
-  const int dbg = a.dbg;
+  const int dbg = SGLM_DBG(a);
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);

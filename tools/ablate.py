@@ -1,5 +1,6 @@
 """Profiling tool: time the fused pass with parts ablated (SGLM_DEBUG_ABLATE bits:
-1 row stage, 2 MFMA, 4 DMA, 8 eta dot product, 16 trivial family arithmetic).
+1 row stage, 2 MFMA, 4 DMA, 8 eta dot product, 16 trivial family arithmetic, 32 no eta store),
+on the ablation build (make -C sparkglm_amd/csrc ablate).
 AN rows, AP columns, AK synth kind, AF/AL family/link."""
 import os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,5 +21,6 @@ print("pass %%.3f ms  %%.0f GB/s  %%.1f TF  wg %%d" %% (ms, n * (8 * p + 8 * nv)
 ''' % ROOT
 for bits in [int(b) for b in os.environ.get("ABITS", "0,1,2,4,3,8,16").split(",")]:
     env = dict(os.environ, SGLM_DEBUG_ABLATE=str(bits))
+    env.setdefault("SGLM_LIB", os.path.join(ROOT, "sparkglm_amd", "lib_ablate", "libsglm_hip.so"))  # make ablate
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     print(f"ablate={bits:3d}: {out.stdout.strip()} {out.stderr[-300:] if out.returncode else ''}", flush=True)

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -336,12 +337,13 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, si, lane);
   }
   if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(1);
-  // Iteration blk runs the MFMA phase of block blk (skipped for blk = b0-1) and the row
-  // stage of block blk+1.
-#pragma unroll 1
-  for (int64_t blk = b0 - 1; blk < b1; ++blk) {
+  // Iteration blk runs the MFMA phase of block blk and the row stage of block blk+1.  The
+  // first iteration (blk = b0-1: row stage of b0 only) is peeled so that the steady-state loop
+  // carries no branch around its MFMA phases (HG: has_gram, compile-time).
+  auto iteration = [&](int64_t blk, auto HG) {
     const int cur = (int)((blk - b0) & 1);  // buffers of block blk; block blk+1 uses cur ^ 1
-    const bool has_gram = blk >= b0 && do_gram;
+    constexpr bool has_gram_ct = decltype(HG)::value;
+    const bool has_gram = has_gram_ct && do_gram;
     const bool has_next = blk + 1 < b1;
     SGLM_STAMP(0);
     if constexpr (G::NA > 0) {
@@ -387,7 +389,10 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     SGLM_STAMP(6);
     if (issuer && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
     SGLM_STAMP(7);
-  }
+  };
+  if (b0 < b1) iteration(b0 - 1, std::false_type{});
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; ++blk) iteration(blk, std::true_type{});
   if (row_wave) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue: this workgroup's partial (tile t of wave wv: see gram_steps) ----

@@ -143,7 +143,9 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
     __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
 }
 
-template <int P16, int FAM, int LNK>
+// IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
+// IRLS = false instantiation, so the iterations' main loop carries none of their branches.
+template <int P16, int FAM, int LNK, bool IRLS>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
@@ -156,7 +158,8 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   const int64_t gw = (int64_t)blockIdx.x * G::NW + wv, nwt = (int64_t)gridDim.x * G::NW;
   const int64_t b0 = nb * gw / nwt, b1 = nb * (gw + 1) / nwt;
   const int ngrp_stored = ((a.p + 7) / 8 * 8) / G::CPI;  // X stores whole column octets
-  const bool irls = a.mode == MODE_IRLS;
+  constexpr bool irls = IRLS;
+  const int mode = IRLS ? (int)MODE_IRLS : a.mode;
   const bool has_eta = irls && a.eta_out != nullptr;
 
   // per-lane parts of the DMA source addresses: lane -> (column cc of the group, row pair j);
@@ -246,7 +249,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
         else
-          pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2);
+          pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2);
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;
@@ -342,23 +345,31 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   }
 }
 
+template <int P16, int FAM, int LNK>
+void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st) {
+  if (a.mode == MODE_IRLS)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true>), gr, bl, 0, st, a);
+  else
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false>), gr, bl, 0, st, a);
+}
+
 template <int P16>
 hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st) {
   const dim3 gr(grid), bl(64 * NGeo<P16>::NW);
   const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_LOGIT>(a, gr, bl, st);
   else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_PROBIT>(a, gr, bl, st);
   else if (fam == FAM_BINOMIAL)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_CLOGLOG>(a, gr, bl, st);
   else if (fam == FAM_GAUSSIAN)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_GAUSSIAN, LNK_IDENTITY>(a, gr, bl, st);
   else if (fam == FAM_POISSON)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_POISSON, LNK_LOG>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_POISSON, LNK_LOG>(a, gr, bl, st);
   else if (fam == FAM_GAMMA)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM_GAMMA, LNK_INVERSE>), gr, bl, 0, st, a);
+    launch_narrow_fl<P16, FAM_GAMMA, LNK_INVERSE>(a, gr, bl, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

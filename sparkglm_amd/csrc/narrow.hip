@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 
     NSTAMP(2);
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
-    if (do_gram) {
+    if (do_gram && P16 > 2) {
 #pragma unroll
       for (int s = 0; s < NRB / 4; ++s) {
         const int r = 4 * s + rq;
@@ -276,6 +276,51 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
           for (int bj = 0; bj <= bi; ++bj, ++t)
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+      }
+    }
+    if (do_gram && P16 <= 2) {
+      // p <= 32 (3 MFMAs per k-step): software-pipelined -- k-step s+1's operands are read from
+      // LDS before k-step s's MFMAs issue, so their latency hides under the MFMA pipe.  (At
+      // p > 32, 10 MFMAs per k-step already cover it; measured +4.8 % there, not kept.)
+      double xv[P16], wr, wzr;
+      {
+        const double* base = xs + cl * NRB + (rq ^ fcl);
+        wr = wl[G::OFF_W + rq];
+        wzr = wl[G::OFF_W + NRB + rq];
+#pragma unroll
+        for (int b = 0; b < P16; ++b) xv[b] = base[G::BSTR * b];
+      }
+#pragma unroll
+      for (int s = 0; s < NRB / 4; ++s) {
+        double xn[P16], wrn = 0.0, wzrn = 0.0;
+        if (s + 1 < NRB / 4) {
+          const int r = 4 * (s + 1) + rq;
+          const double* base = xs + cl * NRB + (r ^ fcl);
+          wrn = wl[G::OFF_W + r];
+          wzrn = wl[G::OFF_W + NRB + r];
+#pragma unroll
+          for (int b = 0; b < P16; ++b) xn[b] = base[G::BSTR * b];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double av[P16];
+#pragma unroll
+        for (int b = 0; b < P16; ++b) {
+          av[b] = xv[b] * wr;
+          xz[b] += xv[b] * wzr;
+        }
+        int t = 0;
+#pragma unroll
+        for (int bi = 0; bi < P16; ++bi)
+#pragma unroll
+          for (int bj = 0; bj <= bi; ++bj, ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < NRB / 4) {
+#pragma unroll
+          for (int b = 0; b < P16; ++b) xv[b] = xn[b];
+          wr = wrn;
+          wzr = wzrn;
+        }
       }
     }
     // every LDS read of this buffer has returned before the DMA may overwrite it

@@ -300,23 +300,28 @@ __global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a
   }
 }
 
-// Row stage: thread per row PAIR (16-byte loads of two adjacent rows of each column),
-// columns streamed in order with four partial sums per row.
+// Row stage: thread per row QUAD (two 16-byte loads of four adjacent rows of each column: a
+// wave reads 2 KiB contiguous per column), columns streamed in order with four partial sums
+// per row (the per-row summation order does not depend on the rows per thread).
 template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
+#ifndef SGLM_WIDE_RPT
+#define SGLM_WIDE_RPT 4
+#endif
+  constexpr int RPT = SGLM_WIDE_RPT;  // rows per thread (even, divides 32)
   __shared__ double red[4][2];
-  const int64_t np2 = a.n_pad / 2;  // row pairs (n_pad is even)
-  const int64_t per = (np2 + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = per * blockIdx.x, hi = (lo + per < np2) ? lo + per : np2;
+  const int64_t nq = a.n_pad / RPT;  // row quads (n_pad is a multiple of 32)
+  const int64_t per = (nq + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = (lo + per < nq) ? lo + per : nq;
   double s_dev = 0.0, s_aux = 0.0;
-  for (int64_t i2 = lo + threadIdx.x; i2 < hi; i2 += blockDim.x) {
-    const int64_t i = 2 * i2;
-    double eta[2] = {0.0, 0.0};
+  for (int64_t iq = lo + threadIdx.x; iq < hi; iq += blockDim.x) {
+    const int64_t i = RPT * iq;
+    double eta[RPT] = {};
     if (a.mode == MODE_IRLS) {
-      double e[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+      double e[RPT][4] = {};
       if (a.proc.on) {  // procedural design: same partial-sum order as the resident image
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+        for (int r = 0; r < RPT; ++r) {
           int j = 0;
           for (; j + 4 <= a.p; j += 4)
 #pragma unroll
@@ -326,27 +331,32 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
       } else {
         const double* xc = a.X + i;
         int j = 0;
-#pragma unroll 2
         for (; j + 4 <= a.p; j += 4)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const double2 v = *(const double2*)(xc + (int64_t)(j + q) * a.ld);
             const double b = a.beta[j + q];
-            e[0][q] += v.x * b;
-            e[1][q] += v.y * b;
+#pragma unroll
+            for (int h = 0; h < RPT / 2; ++h) {
+              const double2 v = *(const double2*)(xc + (int64_t)(j + q) * a.ld + 2 * h);
+              e[2 * h][q] += v.x * b;
+              e[2 * h + 1][q] += v.y * b;
+            }
           }
         for (; j < a.p; ++j) {
-          const double2 v = *(const double2*)(xc + (int64_t)j * a.ld);
-          e[0][0] += v.x * a.beta[j];
-          e[1][0] += v.y * a.beta[j];
+#pragma unroll
+          for (int h = 0; h < RPT / 2; ++h) {
+            const double2 v = *(const double2*)(xc + (int64_t)j * a.ld + 2 * h);
+            e[2 * h][0] += v.x * a.beta[j];
+            e[2 * h + 1][0] += v.y * a.beta[j];
+          }
         }
       }
 #pragma unroll
-      for (int r = 0; r < 2; ++r) eta[r] = (e[r][0] + e[r][1]) + (e[r][2] + e[r][3]);
+      for (int r = 0; r < RPT; ++r) eta[r] = (e[r][0] + e[r][1]) + (e[r][2] + e[r][3]);
     }
-    double w[2] = {0.0, 0.0}, wz[2] = {0.0, 0.0};
+    double w[RPT] = {}, wz[RPT] = {};
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < RPT; ++r) {
       const int64_t row = i + r;
       if (row < a.n) {
         const double y = a.y[row];
@@ -361,8 +371,11 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
         pass_row(FAM, LNK, a.mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w[r], wz[r], s_dev, s_aux);
       }
     }
-    *(double2*)(a.w + i) = double2{w[0], w[1]};
-    *(double2*)(a.wz + i) = double2{wz[0], wz[1]};
+#pragma unroll
+    for (int h = 0; h < RPT / 2; ++h) {
+      *(double2*)(a.w + i + 2 * h) = double2{w[2 * h], w[2 * h + 1]};
+      *(double2*)(a.wz + i + 2 * h) = double2{wz[2 * h], wz[2 * h + 1]};
+    }
   }
   for (int o = 1; o < 64; o <<= 1) {
     s_dev += __shfl_xor(s_dev, o);

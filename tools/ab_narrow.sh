@@ -1,3 +1,4 @@
+# A/B of narrow-pass (p <= 64) builds: sparkglm_amd/lib_ab/base.so vs the in-tree library, then the GPU tests.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export AB_LIBS=sparkglm_amd/lib_ab/base.so,sparkglm_amd/lib/libsglm_hip.so AB_REPS=4

@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     if (do_gram && P16 <= 2) {
       // p <= 32 (3 MFMAs per k-step): software-pipelined -- k-step s+1's operands are read from
       // LDS before k-step s's MFMAs issue, so their latency hides under the MFMA pipe.  (At
-      // p > 32, 10 MFMAs per k-step already cover it; measured +4.8 % there, not kept.)
+      // p > 32, 10 MFMAs per k-step already cover it; measured +1.4 % there, mean of 5, not kept.)
       double xv[P16], wr, wzr;
       {
         const double* base = xs + cl * NRB + (rq ^ fcl);

@@ -11,8 +11,10 @@ the X'WX / X'Wz Gramian on fp64 MFMA) + the all-reduce over ranks + the p x p so
                   [--workload logit256|poisson64|gamma2048|logit512|logit512r|logit1b|lm20]
                   [--rows R] [--p P]
 
-N > 1 is launched by torch.distributed.run (one process per GPU); each rank holds its
-own 100M-row shard (weak scaling) and the per-iteration Gram all-reduce runs on RCCL
+N > 1 runs one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) each process is
+one rank; a plain `python bench.py --gpus N` launches those N rank processes itself (through
+torch.distributed.run, before anything touches the GPU) and exits with their status.  Each rank
+holds its own 100M-row shard (weak scaling) and the per-iteration Gram all-reduce runs on RCCL
 over xGMI inside the engine.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -117,7 +119,42 @@ def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
         return None
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def needs_launch(env, gpus: int) -> bool:
+    """True when this process must spawn the N rank processes itself (no launcher around it)."""
+    return gpus > 1 and "WORLD_SIZE" not in env
+
+
+def launch_cmd(gpus: int, argv, port: int):
+    """The torch.distributed.run command of the N ranks (one process per GPU, rendezvous on
+    127.0.0.1); every rank re-runs this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Run the N ranks as child processes (the parent never initialises the GPU) and return the
+    first non-zero exit status, else 0.  Rank 0's JSON line reaches stdout unchanged."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    log(f"launching {gpus} rank processes (torch.distributed.run)")
+    rc = subprocess.call(launch_cmd(gpus, argv, _free_port()), env=env)
+    if rc != 0:
+        log(f"rank processes failed with exit status {rc}")
+    return rc
+
+
 def main() -> int:
+    if needs_launch(os.environ, _gpus_arg(sys.argv[1:])):
+        return launch_ranks(_gpus_arg(sys.argv[1:]), sys.argv[1:])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -287,6 +324,12 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _gpus_arg(argv) -> int:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    return ap.parse_known_args(argv)[0].gpus
 
 
 def attach_comm(eng, args, world: int, rank: int, dist_on: bool, shared: bool) -> None:

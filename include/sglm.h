@@ -10,6 +10,10 @@
  *   sglm_set_data        replaces utils.dataFrameToMatrix / dfToDenseMatrix
  *                        (utils.scala:36-49) + the per-action re-conversion: one upload,
  *                        X stays resident in HBM across iterations and fits.
+ *   sglm_reserve +       the same, partition by partition (dataFrameToMatrix builds one
+ *   sglm_set_rows        DenseMatrix per partition, utils.scala:36-39; GLM.scala:576-578):
+ *                        blocks of rows -- each within a JVM array's 2^31 elements -- staged
+ *                        through pinned buffers into the reserved shard.
  *   sglm_fit_glm         replaces GLM.fitSingleBinomial (GLM.scala:254-315) and
  *                        GLM.fitMultipleBinomial (GLM.scala:410-468); output = PreGLM
  *                        (GLM.scala:25-33).
@@ -18,8 +22,12 @@
  *                        (LM.scala:10-14) + stdErr/sigma.
  *   sglm_irls_pass       one IRLS pass (zwCreateBinomial + wlsComponents, GLM.scala:
  *                        359-395, utils.scala:110-126) for tests and benchmarks.
- *   sglm_predict         replaces LM.predictSingle/predictMultiple's newX * coefs
- *                        (LM.scala:39-61).
+ *   sglm_predict_new     replaces LM.predictSingle/predictMultiple's newX * coefs
+ *                        (LM.scala:39-61) on new rows, without evicting the resident shard;
+ *                        response scale (mu = unlink(eta)) for GLMs.
+ *   sglm_create_multi    one process owning several GPUs (the single Spark driver that calls
+ *                        GLM.fit / LM.fit, GLM.scala:587, LM.scala:254): row shards per device,
+ *                        one RCCL group all-reduce (ncclCommInitAll) per iteration.
  *   sglm_glm_summary / sglm_lm_summary
  *                        the printed summaries of GLM.summary (GLM.scala:998-1025) and
  *                        SummaryLM (LM.scala:66-137), produced host-side in C++.
@@ -31,9 +39,10 @@
  *   - Matrices are column-major fp64 (Breeze DenseMatrix layout): element (i,j) at
  *     X[i + j*ldx].  The caller keeps ownership of every pointer it passes; the engine
  *     copies into device memory it owns until sglm_destroy.
- *   - One engine handle drives one HIP device.  Multi-GPU = one process (or thread) per
- *     device, each holding its row shard, joined by a communicator (RCCL over xGMI, or a
- *     caller-supplied all-reduce).  Every rank receives identical results.
+ *   - A handle from sglm_create drives one HIP device; one from sglm_create_multi drives
+ *     several (row shards, Spark's slicing [d n/D, (d+1) n/D)).  Across processes (or host
+ *     threads, one handle each) shards join a communicator: RCCL over xGMI, a caller-supplied
+ *     all-reduce, or the in-process sglm_local_allreduce.  Every rank receives identical results.
  *   - Handles are not thread-safe; distinct handles may be used concurrently.
  */
 #ifndef SGLM_H
@@ -46,7 +55,7 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 1
+#define SGLM_ABI_VERSION 2
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -70,6 +79,9 @@ enum sglm_init {
   SGLM_INIT_SINGLE = 0,  /* fitSingleBinomial: mu = mean(y) directly (GLM.scala:263, 282-290) */
   SGLM_INIT_MULTIPLE = 1 /* fitMultipleBinomial: mu = unlink(link(mean(y))) (GLM.scala:370-371) */
 };
+
+/* Prediction scale (R's predict(type = "link" | "response")). */
+enum sglm_predict_type { SGLM_PREDICT_LINK = 0, SGLM_PREDICT_RESPONSE = 1 };
 
 typedef struct sglm_engine sglm_engine;
 
@@ -125,6 +137,10 @@ typedef struct {
   int wide_panels;          /* wide path: 128-column panels */
   double row_kernel_ms;     /* wide path: total time of the row kernel (eta, w, w*z) */
   double gram_kernel_ms;    /* wide path: total time of the panel-pair Gram kernel */
+  double load_ms;           /* host wall time of set_data / set_rows (pinned staging + H2D) */
+  int64_t load_bytes;       /* bytes those calls moved to the device */
+  int ndev;                 /* devices driven by this handle */
+  int rccl_group;           /* multi-device handle reducing over RCCL (1) or on the host (0) */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
@@ -136,6 +152,13 @@ int sglm_abi_version(void);
 const char *sglm_last_error(void);
 int sglm_device_count(int *count);
 int sglm_create(int device, sglm_engine **out);
+/* One handle over devs[0..ndev): rows are sharded contiguously across the devices; each
+ * iteration's packed partials are all-reduced by one RCCL group call over communicators from
+ * ncclCommInitAll (distinct devices) or summed on the host in device order (a device listed
+ * twice: rehearsal on fewer GPUs).  Every call below accepts it, except sglm_set_data_device,
+ * sglm_set_comm and sglm_set_comm_rccl. */
+int sglm_create_multi(const int *devs, int ndev, sglm_engine **out);
+int sglm_handle_devices(sglm_engine *h, int *ndev);
 void sglm_destroy(sglm_engine *h);
 
 /* ---- data (utils.dataFrameToMatrix replacement) ------------------------------ */
@@ -146,6 +169,15 @@ int sglm_set_data(sglm_engine *h, const double *X, int64_t n, int64_t p, int64_t
 int sglm_set_data_device(sglm_engine *h, const double *dX, int64_t n, int64_t p, int64_t ldx,
                          const double *dy, const double *dm, const double *doffset,
                          const double *dprior);
+/* Partition-wise ingest.  sglm_reserve allocates the shard (n rows x p columns, plus the
+ * optional vectors) without filling it; sglm_set_rows then copies rows [row0, row0+nrows)
+ * from a host column-major block (leading dimension ldx >= nrows; vectors of nrows) through
+ * two pinned staging buffers (pageable memory never reaches the DMA engine).  Blocks may
+ * arrive in any order and must not overlap; a fit requires every reserved row written.
+ * m / offset / prior must be passed exactly when reserved. */
+int sglm_reserve(sglm_engine *h, int64_t n, int64_t p, int has_m, int has_offset, int has_prior);
+int sglm_set_rows(sglm_engine *h, int64_t row0, int64_t nrows, const double *X, int64_t ldx,
+                  const double *y, const double *m, const double *offset, const double *prior);
 /* Generate this rank's row shard [row0, row0+n) of the seeded synthetic design directly
  * in HBM (bench / scale tests).  kind: 0 = logit design (y in {0,1}), 1 = gaussian (LM),
  * 2 = poisson counts + offset + prior, 3 = gamma design (positive X, y > 0).  Column 0
@@ -187,6 +219,16 @@ int sglm_irls_iterations(sglm_engine *h, const sglm_glm_opts *opts, double *beta
 
 /* eta = X * beta (+ offset if add_offset) for the resident rows, written to out [n_local]. */
 int sglm_predict(sglm_engine *h, const double *beta, int add_offset, double *out);
+/* The same on the link (eta) or response (mu = unlink(eta, m), m = the resident trials or 1)
+ * scale of family/link: fitted values of the resident rows. */
+int sglm_predict_glm(sglm_engine *h, const double *beta, int family, int link, int type, int add_offset,
+                     double *out);
+/* Score NEW rows (LM.predict, LM.scala:29-61; GLM response-scale prediction): X column-major
+ * n x p (ldx >= n), optional offset / m (NULL: 0 / 1).  Streams X through a device scratch in
+ * chunks; the resident training shard is untouched. */
+int sglm_predict_new(sglm_engine *h, const double *X, int64_t n, int64_t p, int64_t ldx,
+                     const double *beta, const double *offset, const double *m, int family, int link,
+                     int type, double *out);
 
 int sglm_get_stats(sglm_engine *h, sglm_stats *out);
 int sglm_reset_stats(sglm_engine *h);
@@ -207,6 +249,17 @@ int sglm_fit_glm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *co
                           const sglm_glm_opts *opts, sglm_preglm *out);
 int sglm_fit_lm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *comm_ctx,
                          sglm_prelm *out);
+
+/* ---- in-process communicator: N host threads in one process, one handle each ---------
+ * (a JVM driver's thread pool over N single-device handles; the alternative to
+ * sglm_create_multi).  Pass sglm_local_allreduce with sglm_local_comm_rank(c, r) as the
+ * context of rank r to sglm_set_comm (on_device = 0) or sglm_fit_*_external.  The sum runs
+ * in rank order, so every rank gets bitwise the same result. */
+typedef struct sglm_local_comm sglm_local_comm;
+int sglm_local_comm_create(int nranks, sglm_local_comm **out);
+void sglm_local_comm_destroy(sglm_local_comm *c);
+void *sglm_local_comm_rank(sglm_local_comm *c, int rank);
+int sglm_local_allreduce(void *ctx, double *buf, int64_t count, void *stream, int on_device);
 
 /* ---- model objects and printed summaries (host-side, C++) ---------------------- */
 /* GLM.createObj (GLM.scala:59-88) derived fields. */

@@ -54,6 +54,9 @@ def lib():
         _lib.orc_shard_partials.argtypes = [dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, dp,
                                             C.c_int, C.c_int, C.c_int, dp, C.c_double, C.c_double, dp]
         _lib.orc_lu_inverse.argtypes = [dp, C.c_int64]
+        _lib.orc_fit_glm_synth.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64,
+                                           C.POINTER(_Opts), C.POINTER(_Pre)]
+        _lib.orc_synth_rows.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, dp, dp, dp, dp]
         for f in ("orc_norm_cdf", "orc_norm_icdf", "orc_erfinv"):
             getattr(_lib, f).argtypes = [C.c_double]
             getattr(_lib, f).restype = C.c_double
@@ -106,6 +109,33 @@ def fit_glm(X, y, family="binomial", link="logit", *, m=None, offset=None, prior
         raise RuntimeError(f"oracle orc_fit_glm failed rc={rc}")
     return OraclePreGLM(coefs, se, pre.deviance, pre.null_deviance, pre.pearson, pre.loglik,
                         pre.iter, pre.nrow, pre.npart, trace[: pre.iter + 1].copy())
+
+
+def fit_glm_synth(kind, row0, n, p, seed, family="binomial", link="logit", *, tol=1e-6, max_iter=0, npart=1,
+                  nthreads=8, verbose=False, max_trace=256) -> OraclePreGLM:
+    """Streaming fit of rows [row0, row0+n) of the synthetic design (sparkglm_amd.synth), rows
+    regenerated chunk by chunk every iteration (orc_fit_glm_synth): full-size parity without
+    holding X in host RAM."""
+    coefs, se, trace = np.zeros(p), np.zeros(p), np.full(max_trace, np.nan)
+    o = _Opts(FAMILIES[family], LINKS[link], tol, max_iter, int(verbose), npart, nthreads)
+    pre = _Pre(_ptr(coefs), _ptr(se), 0, 0, 0, 0, 0, 0, 0, _ptr(trace), max_trace)
+    rc = lib().orc_fit_glm_synth(int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1)),
+                                 C.byref(o), C.byref(pre))
+    if rc != 0:
+        raise RuntimeError(f"oracle orc_fit_glm_synth failed rc={rc}")
+    return OraclePreGLM(coefs, se, pre.deviance, pre.null_deviance, pre.pearson, pre.loglik,
+                        pre.iter, pre.nrow, pre.npart, trace[: pre.iter + 1].copy())
+
+
+def synth_rows(kind, row0, n, p, seed):
+    """The oracle's C copy of the synthetic generator: (X (n x p, Fortran), y, offset, prior)."""
+    X = np.empty((n, p), order="F")
+    y, off, pr = np.empty(n), np.empty(n), np.empty(n)
+    rc = lib().orc_synth_rows(int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1)),
+                              X.ctypes.data_as(C.POINTER(C.c_double)), _ptr(y), _ptr(off), _ptr(pr))
+    if rc != 0:
+        raise RuntimeError("oracle orc_synth_rows failed")
+    return X, y, (off if kind == 2 else None), (pr if kind == 2 else None)
 
 
 def fit_lm(X, y, npart=1, nthreads=1):

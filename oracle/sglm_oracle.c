@@ -582,6 +582,11 @@ int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx, const
     z[i] = (eta[i] + ((y[i] + (-1.0 * mu[i])) * grad)) + (-1.0 * OFF_(&d, i));
   }
   gram_rows(X, ldx, p, 0, n, w, z, Gm, xtwz);
+  /* fitMultipleBinomial re-derives mu = unlink(link(ybar)) only inside zwCreateBinomial; the null
+     deviance (and the statistics of a fit that stops before its first solve) are taken at
+     mu0 = ybar itself (GLM.scala:424-444). */
+  if (mode == ORC_MODE_INIT_MULTI)
+    for (int64_t i = 0; i < n; ++i) mu[i] = mu0;
   for (int64_t i = 0; i < n; ++i) tmp[i] = unit_dev(family, y[i], mu[i], M_(&d, i), PW_(&d, i));
   s[ORC_S_DEV] = pairwise_sum(tmp, n);
   for (int64_t i = 0; i < n; ++i) {
@@ -619,4 +624,280 @@ pack:
 out:
   free(eta); free(mu); free(w); free(z); free(tmp); free(Gm); free(xtwz);
   return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Streaming ("procedural") fits for designs larger than host RAM (SURVEY.md    */
+/* 8(d): "for sizes beyond host RAM, regenerate rows on the fly from the same    */
+/* generator").  The rows come from the seeded counter-based generator of       */
+/* sparkglm_amd/synth.py (bit-identical: integer splitmix64, IEEE mul/add, no    */
+/* contraction); every IRLS iteration regenerates them chunk by chunk, so only  */
+/* p x p state is kept.  The fit is the single-pass restatement of               */
+/* fitSingleBinomial (GLM.scala:254-315; npart > 1: fitMultipleBinomial's        */
+/* mu = unlink(link(ybar)) first step, GLM.scala:370-371): pass k at beta_k      */
+/* yields dev_k (the loop test, GLM.scala:301-303), pearson / loglik at mu_k     */
+/* (GLM.scala:307-311) and X'W_kX, X'W_kz_k for the next wlsSingle solve         */
+/* (utils.scala:98-107) -- the same quantities the reference derives from its    */
+/* stored mu, since mu_k = unlink(X beta_k + offset).  Sums run in a fixed order */
+/* (64 contiguous row segments, chunks in order inside each) independent of the  */
+/* thread count.                                                                 */
+/* ------------------------------------------------------------------------- */
+static inline uint64_t sm64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+static inline double unif64(uint64_t key) { return (double)(sm64(key) >> 11) * 0x1.0p-53; }
+
+typedef struct {
+  int kind;
+  int64_t p;
+  uint64_t kx, ky, ko, kp;
+  double scale;
+  double *bs; /* beta* of the generator */
+} orc_gen;
+
+static void gen_init(orc_gen *g, int kind, int64_t p, uint64_t seed) {
+  g->kind = kind;
+  g->p = p;
+  g->kx = sm64(seed);
+  g->ky = sm64(seed ^ 0x5555555555555555ULL);
+  g->ko = sm64(seed ^ 0x3333333333333333ULL);
+  g->kp = sm64(seed ^ 0x0F0F0F0F0F0F0F0FULL);
+  g->scale = 1.0 / sqrt((double)p);
+  g->bs = (double *)malloc(sizeof(double) * (size_t)p);
+  for (int64_t j = 0; j < p; ++j) g->bs[j] = kind == 3 ? 0.1 * (double)((j % 5) + 1) : 0.5 * (double)((j % 5) - 2);
+  g->bs[0] = kind == 3 ? 1.0 : -0.25;
+}
+
+/* Rows [gi0, gi0+nr) (global indices) into X (ld rows), y, offset / prior (kind 2). */
+static void gen_rows(const orc_gen *g, int64_t gi0, int64_t nr, double *X, int64_t ld, double *y, double *off,
+                     double *pr) {
+  const int64_t p = g->p;
+  for (int64_t i = 0; i < nr; ++i) {
+    const uint64_t gi = (uint64_t)(gi0 + i);
+    const uint64_t base = g->kx + gi * (uint64_t)p;
+    double eta = 0.0;
+    for (int64_t j = 0; j < p; ++j) {
+      double x;
+      if (j == 0) x = 1.0;
+      else if (g->kind == 3) x = (0.5 + unif64(base + (uint64_t)j)) * g->scale;
+      else x = (2.0 * unif64(base + (uint64_t)j) - 1.0) * g->scale;
+      X[i + j * ld] = x;
+      double prod = x * g->bs[j];
+      eta = eta + prod;
+    }
+    const double u = unif64(g->ky + gi);
+    if (off) off[i] = 0.0;
+    if (pr) pr[i] = 1.0;
+    if (g->kind == 0) {
+      double q = fmin(fmax(0.5 + 0.25 * eta, 0.02), 0.98);
+      y[i] = u < q ? 1.0 : 0.0;
+    } else if (g->kind == 1) {
+      y[i] = eta + (2.0 * u - 1.0);
+    } else if (g->kind == 2) {
+      double lam = fmax(1.0 + 0.5 * eta, 0.1);
+      y[i] = floor(u * 2.0 * lam);
+      if (off) off[i] = (2.0 * unif64(g->ko + gi) - 1.0) * 0.1;
+      if (pr) pr[i] = 0.5 + unif64(g->kp + gi);
+    } else {
+      y[i] = (0.25 + 1.5 * u) / eta;
+    }
+  }
+}
+
+int orc_synth_rows(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, double *X, double *y, double *off,
+                   double *pr) {
+  if (kind < 0 || kind > 3 || n < 0 || p <= 0) return ORC_EINVAL;
+  orc_gen g;
+  gen_init(&g, kind, p, seed);
+  gen_rows(&g, row0, n, X, n, y, off, pr);
+  free(g.bs);
+  return ORC_OK;
+}
+
+#define ORC_NSEG 64
+#define ORC_CH 256
+
+enum { SP_YSUM = 100 };
+
+typedef struct {
+  double *G, *xtwz; /* G: p*p col-major, lower triangle accumulated */
+  double s[ORC_NS], c[ORC_NS]; /* scalar sums with Neumaier compensation terms */
+} seg_acc;
+
+/* Compensated (Neumaier) accumulation: at 1e9 rows a plain running sum of the deviance carries
+ * ~1e-6 of rounding noise -- the size of GLM.scala:281's absolute tol -- so the iteration count
+ * would follow the summation order instead of the fit.  The compensated sum is accurate to
+ * about one ulp of the total. */
+static inline void neumaier(double *s, double *c, double x) {
+  double t = *s + x;
+  if (fabs(*s) >= fabs(x)) *c += (*s - t) + x;
+  else *c += (x - t) + *s;
+  *s = t;
+}
+
+/* One pass over rows [row0, row0+n) of the generated design (see the section comment). */
+static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, int link, int mode,
+                        const double *beta, double mu0, int nthreads, seg_acc *seg) {
+  const int64_t p = g->p;
+  const int has_op = g->kind == 2;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+  {
+    double *X = (double *)malloc(sizeof(double) * ORC_CH * (size_t)p);
+    double *y = (double *)malloc(sizeof(double) * ORC_CH), *off = (double *)malloc(sizeof(double) * ORC_CH);
+    double *pr = (double *)malloc(sizeof(double) * ORC_CH), *w = (double *)malloc(sizeof(double) * ORC_CH);
+    double *z = (double *)malloc(sizeof(double) * ORC_CH), *t = (double *)malloc(sizeof(double) * ORC_CH * ORC_NS);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+      seg_acc *a = &seg[sgi];
+      memset(a->s, 0, sizeof a->s);
+      memset(a->c, 0, sizeof a->c);
+      if (mode != SP_YSUM) {
+        memset(a->G, 0, sizeof(double) * (size_t)(p * p));
+        memset(a->xtwz, 0, sizeof(double) * (size_t)p);
+      }
+      const int64_t lo = part_lo(n, sgi, ORC_NSEG), hi = part_lo(n, sgi + 1, ORC_NSEG);
+      for (int64_t c0 = lo; c0 < hi; c0 += ORC_CH) {
+        const int64_t nr = (hi - c0) < ORC_CH ? (hi - c0) : ORC_CH;
+        gen_rows(g, row0 + c0, nr, X, ORC_CH, y, has_op ? off : NULL, has_op ? pr : NULL);
+        if (mode == SP_YSUM) {
+          neumaier(&a->s[ORC_S_DEV], &a->c[ORC_S_DEV], pairwise_sum(y, nr));
+          continue;
+        }
+        for (int64_t i = 0; i < nr; ++i) {
+          const double oi = has_op ? off[i] : 0.0, pw = has_op ? pr[i] : 1.0;
+          double eta, mu, mud;
+          if (mode == ORC_MODE_IRLS) {
+            eta = 0.0; /* eta_create (GLM.scala:292 / 321-332) */
+            for (int64_t j = 0; j < p; ++j) eta += X[i + j * ORC_CH] * beta[j];
+            eta = eta + oi;
+            mu = unlink_fn(family, link, eta, 1.0);
+            mud = mu;
+          } else { /* eta = link(mu0), offset ignored (GLM.scala:264-270, 429-442) */
+            eta = link_fn(family, link, mu0, 1.0);
+            mu = (mode == ORC_MODE_INIT_SINGLE) ? mu0 : unlink_fn(family, link, eta, 1.0);
+            mud = mu0; /* the null deviance is taken at mu0 itself (GLM.scala:271, 443) */
+          }
+          const double grad = lprime_fn(family, link, mu, 1.0);
+          w[i] = pw * (1.0 / (variance_fn(family, mu, 1.0) * (grad * grad)));
+          z[i] = (eta + ((y[i] + (-1.0 * mu)) * grad)) + (-1.0 * oi);
+          const double r = y[i] + (-1.0 * mud);
+          double *ti = t + i;
+          ti[ORC_S_DEV * ORC_CH] = unit_dev(family, y[i], mud, 1.0, pw);
+          ti[ORC_S_PEARSON * ORC_CH] = pw * (r * r) / variance_fn(family, mud, 1.0);
+          ti[ORC_S_AUX0 * ORC_CH] = 0.0;
+          ti[ORC_S_AUX1 * ORC_CH] = 0.0;
+          ti[ORC_S_BAD * ORC_CH] = 0.0;
+          if (family == ORC_BINOMIAL) {
+            int bad = 0; /* m = 1: Binomial(1, mu).logProbabilityOf(y.toInt) (GLM.scala:140) */
+            ti[ORC_S_LL * ORC_CH] = pw * binom_logpmf(1.0, mud, y[i], &bad);
+            ti[ORC_S_BAD * ORC_CH] = (double)bad;
+          } else if (family == ORC_POISSON) {
+            ti[ORC_S_LL * ORC_CH] = pw * (y[i] * log(mud) - mud - lgamma(y[i] + 1.0));
+          } else if (family == ORC_GAUSSIAN) {
+            ti[ORC_S_LL * ORC_CH] = log(pw);
+          } else {
+            ti[ORC_S_LL * ORC_CH] = pw * log(y[i]);
+            ti[ORC_S_AUX0 * ORC_CH] = pw * (y[i] / mud);
+            ti[ORC_S_AUX1 * ORC_CH] = pw * log(mud);
+          }
+          ti[ORC_S_SUMW * ORC_CH] = pw;
+        }
+        for (int k = 0; k < ORC_NS; ++k)
+          if (k != ORC_S_AUX2) neumaier(&a->s[k], &a->c[k], pairwise_sum(t + k * ORC_CH, nr));
+        gram_rows(X, ORC_CH, p, 0, nr, w, z, a->G, a->xtwz);
+      }
+    }
+    free(X); free(y); free(off); free(pr); free(w); free(z); free(t);
+  }
+}
+
+static void seg_total(const seg_acc *seg, int64_t p, int with_gram, double *G, double *xtwz, double *s) {
+  double cs[ORC_NS] = {0};
+  memset(s, 0, sizeof(double) * ORC_NS);
+  if (with_gram) {
+    memset(G, 0, sizeof(double) * (size_t)(p * p));
+    memset(xtwz, 0, sizeof(double) * (size_t)p);
+  }
+  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+    for (int k = 0; k < ORC_NS; ++k) {
+      neumaier(&s[k], &cs[k], seg[sgi].s[k]);
+      neumaier(&s[k], &cs[k], seg[sgi].c[k]);
+    }
+    if (!with_gram) continue;
+    for (int64_t j = 0; j < p; ++j)
+      for (int64_t i = j; i < p; ++i) G[i + j * p] += seg[sgi].G[i + j * p];
+    for (int64_t j = 0; j < p; ++j) xtwz[j] += seg[sgi].xtwz[j];
+  }
+  for (int k = 0; k < ORC_NS; ++k) s[k] += cs[k];
+  if (with_gram) symmetrize_lower(G, p);
+}
+
+int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, const orc_opts *o,
+                      orc_preglm *out) {
+  if (kind < 0 || kind > 3 || n <= 0 || p <= 0) return ORC_EINVAL;
+  orc_gen g;
+  gen_init(&g, kind, p, seed);
+  seg_acc *seg = (seg_acc *)calloc(ORC_NSEG, sizeof(seg_acc));
+  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+    seg[sgi].G = (double *)calloc((size_t)(p * p), sizeof(double));
+    seg[sgi].xtwz = (double *)calloc((size_t)p, sizeof(double));
+  }
+  double *Gm = malloc(sizeof(double) * (size_t)(p * p)), *xtwz = malloc(sizeof(double) * (size_t)p);
+  double *coefs = calloc((size_t)p, sizeof(double)), *diag_design = calloc((size_t)p, sizeof(double));
+  double s[ORC_NS];
+  const double fac = family_dev_factor(o->family);
+  int rc = ORC_OK;
+
+  stream_pass(&g, row0, n, o->family, o->link, SP_YSUM, NULL, 0.0, o->nthreads, seg);
+  seg_total(seg, p, 0, NULL, NULL, s);
+  const double ymean = s[ORC_S_DEV] / (double)n; /* GLM.scala:263 / 423 */
+  const int init = o->npart > 1 ? ORC_MODE_INIT_MULTI : ORC_MODE_INIT_SINGLE;
+  stream_pass(&g, row0, n, o->family, o->link, init, NULL, ymean, o->nthreads, seg);
+  seg_total(seg, p, 1, Gm, xtwz, s);
+  double dev = fac * s[ORC_S_DEV], null_dev = dev, dev_old, deltad = 1.0;
+  int iter = 0;
+  if (out->dev_trace && out->max_trace > 0) out->dev_trace[0] = dev;
+  while (fabs(deltad) > o->tol) { /* GLM.scala:281 / 452 */
+    if (o->max_iter > 0 && iter >= o->max_iter) break;
+    rc = wls_solve(Gm, xtwz, p, coefs, diag_design); /* wlsSingle (utils.scala:98-107) */
+    if (rc) goto done;
+    stream_pass(&g, row0, n, o->family, o->link, ORC_MODE_IRLS, coefs, ymean, o->nthreads, seg);
+    seg_total(seg, p, 1, Gm, xtwz, s);
+    dev_old = dev;
+    dev = fac * s[ORC_S_DEV];
+    deltad = dev - dev_old;
+    iter = iter + 1;
+    if (out->dev_trace && iter < out->max_trace) out->dev_trace[iter] = dev;
+    if (o->verbose) { printf("%d\t%.17g\n", iter, deltad); fflush(stdout); }
+  }
+  if (s[ORC_S_BAD] > 0) { rc = ORC_EINVAL; goto done; }
+  {
+    double ll = s[ORC_S_LL];
+    if (o->family == ORC_GAUSSIAN) {
+      ll = -((double)n / 2.0) * (log(2.0 * M_PI * dev / (double)n) + 1.0) + 0.5 * s[ORC_S_LL];
+    } else if (o->family == ORC_GAMMA) {
+      double sw = s[ORC_S_SUMW], disp = dev / sw, a = 1.0 / disp;
+      ll = (a - 1.0) * s[ORC_S_LL] - s[ORC_S_AUX0] / disp - (lgamma(a) + a * log(disp)) * sw - a * s[ORC_S_AUX1];
+    }
+    memcpy(out->coefs, coefs, sizeof(double) * (size_t)p);
+    memcpy(out->stderr_, diag_design, sizeof(double) * (size_t)p);
+    out->deviance = dev;
+    out->null_deviance = null_dev;
+    out->pearson = s[ORC_S_PEARSON];
+    out->loglik = ll;
+    out->iter = iter;
+    out->nrow = (double)n;
+    out->npart = o->npart > 0 ? o->npart : 1;
+  }
+done:
+  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) { free(seg[sgi].G); free(seg[sgi].xtwz); }
+  free(seg); free(Gm); free(xtwz); free(coefs); free(diag_design); free(g.bs);
+  return rc;
 }

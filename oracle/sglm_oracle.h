@@ -73,6 +73,16 @@ int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx,
                        int family, int link, int mode, const double *beta, double mu0, double ybar,
                        double *packed);
 
+/* Streaming fit of the seeded synthetic design (sparkglm_amd/synth.py generator, kinds 0-3,
+ * rows [row0, row0+n)), regenerated chunk by chunk on every IRLS iteration: full-scale
+ * parity without holding X in host RAM.  npart > 1 selects the
+ * fitMultipleBinomial first step; m = 1.  Same outputs as orc_fit_glm. */
+int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, const orc_opts *opts,
+                      orc_preglm *out);
+/* The generator itself (X column-major with ld = n; offset / prior only for kind 2, may be NULL). */
+int orc_synth_rows(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, double *X, double *y,
+                   double *offset, double *prior);
+
 /* Breeze inv() semantics: LU with partial pivoting (dgetrf) + inverse (dgetri). In place, col-major. */
 int orc_lu_inverse(double *A, int64_t p);
 

@@ -29,8 +29,11 @@ EXPORTS = [
     "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
     "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
-    "sglm_pval_normal", "sglm_pval_t",
+    "sglm_pval_normal", "sglm_pval_t", "sglm_create_multi", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
+    "sglm_predict_glm", "sglm_predict_new", "sglm_local_comm_create", "sglm_local_comm_destroy",
+    "sglm_local_comm_rank", "sglm_local_allreduce",
 ]
+PREDICT_LINK, PREDICT_RESPONSE = 0, 1
 
 dp = C.POINTER(C.c_double)
 
@@ -56,7 +59,8 @@ class Stats(C.Structure):
                 ("last_pass_ms", C.c_double), ("comm_ms", C.c_double), ("solve_ms", C.c_double),
                 ("n_local", C.c_int64), ("p", C.c_int64), ("workgroups", C.c_int), ("kernel_variant", C.c_int),
                 ("path", C.c_int), ("wide_panels", C.c_int), ("row_kernel_ms", C.c_double),
-                ("gram_kernel_ms", C.c_double)]
+                ("gram_kernel_ms", C.c_double), ("load_ms", C.c_double), ("load_bytes", C.c_int64),
+                ("ndev", C.c_int), ("rccl_group", C.c_int)]
 
 
 class GlmDerived(C.Structure):
@@ -136,6 +140,17 @@ def load():
         "sglm_java_double_string": ([C.c_double, C.c_char_p, C.c_int64], C.c_int64),
         "sglm_pval_normal": ([C.c_double], C.c_double),
         "sglm_pval_t": ([C.c_double, C.c_double], C.c_double),
+        "sglm_create_multi": ([C.POINTER(C.c_int), C.c_int, E], C.c_int),
+        "sglm_handle_devices": ([h, C.POINTER(C.c_int)], C.c_int),
+        "sglm_reserve": ([h, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int], C.c_int),
+        "sglm_set_rows": ([h, C.c_int64, C.c_int64, dp, C.c_int64, dp, dp, dp, dp], C.c_int),
+        "sglm_predict_glm": ([h, dp, C.c_int, C.c_int, C.c_int, C.c_int, dp], C.c_int),
+        "sglm_predict_new": ([h, dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, C.c_int, C.c_int, C.c_int, dp],
+                             C.c_int),
+        "sglm_local_comm_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+        "sglm_local_comm_destroy": ([C.c_void_p], None),
+        "sglm_local_comm_rank": ([C.c_void_p, C.c_int], C.c_void_p),
+        "sglm_local_allreduce": ([C.c_void_p, dp, C.c_int64, C.c_void_p, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         if os.environ.get("SGLM_LIB") and not hasattr(lib, name):

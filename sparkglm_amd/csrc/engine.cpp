@@ -17,19 +17,24 @@
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sglm.h"
 #include "common.hpp"
 #include "driver.hpp"
 #include "kernels.hpp"
+#include "solve.hpp"
 
 using namespace sglm;
 
@@ -62,6 +67,31 @@ struct Comm {
   int nranks = 1;
   double ms = 0.0;
 };
+
+// Copy a column-major host block (rows x cols, leading dimension sld) into a packed buffer,
+// on several threads for large blocks (the pageable -> pinned leg of the ingest path).
+void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_t cols) {
+  const int64_t total = rows * cols;
+  const int hw = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const int nt = total >= ((int64_t)2 << 20) ? hw : 1;  // >= 16 MiB: split the copy
+  auto part = [&](int t) {
+    if (cols >= nt) {
+      for (int64_t c = t; c < cols; c += nt) std::memcpy(dst + c * rows, src + c * sld, sizeof(double) * rows);
+    } else {
+      const int64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
+      for (int64_t c = 0; c < cols; ++c)
+        std::memcpy(dst + c * rows + r0, src + c * sld + r0, sizeof(double) * (size_t)(r1 - r0));
+    }
+  };
+  if (nt == 1) {
+    part(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -100,8 +130,32 @@ struct sglm_engine : public Backend {
   int64_t passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
+  // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
+  static constexpr int64_t STAGE_DOUBLES = (int64_t)8 << 20;  // 64 MiB each
+  double* hstage[2] = {nullptr, nullptr};
+  hipEvent_t evstage[2] = {nullptr, nullptr};
+  int stage_k = 0;
+  int64_t rows_loaded = 0;  // rows written since the shard was reserved
+  double load_ms = 0.0;     // host wall time in set_data / set_rows (staging + H2D)
+  int64_t load_bytes = 0;
+  // new-row scoring (sglm_predict_new): a device scratch, separate from the resident shard
+  double *dxs = nullptr, *dvs = nullptr, *dms = nullptr, *dos = nullptr;
+  int64_t xs_cap = 0, vs_cap = 0;
+  // single-process multi-device handle (sglm_create_multi): the shards' engines; this handle
+  // then only routes and reduces (one process owns all GPUs, as SURVEY 8(b) asks)
+  std::vector<sglm_engine*> subs;
+  std::vector<int64_t> sub_lo;       // first global row of each shard
+  std::vector<ncclComm_t> gcomms;    // ncclCommInitAll over distinct devices (else host sums)
+  int64_t g_n = 0;                   // group: total rows
+  bool group() const { return !subs.empty(); }
 
-  ~sglm_engine() override { release(); }
+  ~sglm_engine() override {
+    for (sglm_engine* s : subs) delete s;
+    for (ncclComm_t c : gcomms) (void)ncclCommDestroy(c);
+    subs.clear();
+    gcomms.clear();
+    release();
+  }
 
   void free_data() {
     for (double** ptr : {&dX, &dy, &dm, &doff, &dprior, &deta, &dw, &dwz}) {
@@ -109,14 +163,22 @@ struct sglm_engine : public Backend {
       *ptr = nullptr;
     }
     n = p = n_pad = nblocks = 0;
+    rows_loaded = 0;
     procx = ProcX{};
   }
   void release() {
     (void)hipSetDevice(device);
     free_data();
-    for (double** ptr : {&dbeta, &dpart, &dred, &dsmall, &dgp, &drp}) {
+    for (double** ptr : {&dbeta, &dpart, &dred, &dsmall, &dgp, &drp, &dxs, &dvs, &dms, &dos}) {
       if (*ptr) (void)hipFree(*ptr);
       *ptr = nullptr;
+    }
+    xs_cap = vs_cap = 0;
+    for (int k = 0; k < 2; ++k) {
+      if (hstage[k]) (void)hipHostFree(hstage[k]);
+      if (evstage[k]) (void)hipEventDestroy(evstage[k]);
+      hstage[k] = nullptr;
+      evstage[k] = nullptr;
     }
     free_schedule();
     part_cap = red_cap = gp_cap = rp_cap = 0;
@@ -138,8 +200,8 @@ struct sglm_engine : public Backend {
     st = nullptr;
   }
 
-  int64_t ncols() const override { return p; }
-  int npart() const override { return comm.nranks; }
+  int64_t ncols() const override { return group() ? subs[0]->p : p; }
+  int npart() const override { return group() ? (int)subs.size() : comm.nranks; }
 
   // ---- communicator helpers ----
   int allreduce_device(double* dbuf, int64_t count) {
@@ -366,9 +428,153 @@ struct sglm_engine : public Backend {
     return ensure_workspace();
   }
 
+  // ---- ingest: pageable host -> pinned staging -> HBM ----
+  int ensure_staging() {
+    if (hstage[0]) return SGLM_OK;
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(hipHostMalloc(&hstage[k], sizeof(double) * STAGE_DOUBLES, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&evstage[k], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(evstage[k], st));
+    }
+    return SGLM_OK;
+  }
+  // Column-major host block (rows x cols, leading dimension sld) -> device (leading dimension
+  // dld) through the two pinned buffers: the CPU packs one while the DMA engine drains the
+  // other.  Pageable memory is never handed to the DMA engine directly.
+  int h2d_block(double* dst, int64_t dld, const double* src, int64_t sld, int64_t rows, int64_t cols) {
+    if (rows <= 0 || cols <= 0) return SGLM_OK;
+    int rc = ensure_staging();
+    if (rc) return rc;
+    const int64_t rchunk = std::min<int64_t>(rows, STAGE_DOUBLES);
+    for (int64_t r0 = 0; r0 < rows; r0 += rchunk) {
+      const int64_t rr = std::min(rchunk, rows - r0);
+      const int64_t cchunk = std::max<int64_t>(1, STAGE_DOUBLES / rr);
+      for (int64_t c0 = 0; c0 < cols; c0 += cchunk) {
+        const int64_t cc = std::min(cchunk, cols - c0);
+        const int k = stage_k;
+        stage_k ^= 1;
+        HIPCHK(hipEventSynchronize(evstage[k]));  // the copy that last read this buffer is done
+        pack_cols(hstage[k], src + r0 + c0 * sld, sld, rr, cc);
+        HIPCHK(hipMemcpy2DAsync(dst + r0 + c0 * dld, sizeof(double) * (size_t)dld, hstage[k], sizeof(double) * rr,
+                                sizeof(double) * rr, (size_t)cc, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(evstage[k], st));
+      }
+    }
+    return SGLM_OK;
+  }
+
+  // Rows [row0, row0 + nr) of the reserved shard from host memory (sglm_set_rows).
+  int set_rows(int64_t row0, int64_t nr, const double* X, int64_t ldx, const double* yv, const double* mv,
+               const double* ov, const double* pv) {
+    HIPCHK(hipSetDevice(device));
+    if (p <= 0 || procx.on) {
+      set_error("requirement failed: sglm_reserve the shard before sglm_set_rows");
+      return SGLM_EINVAL;
+    }
+    if (row0 < 0 || nr < 0 || row0 + nr > n || (nr > 0 && (!X || !yv || ldx < nr))) {
+      set_error("requirement failed: 0 <= row0, row0 + nrows <= reserved rows, X and y non-null, ldx >= nrows");
+      return SGLM_EINVAL;
+    }
+    if ((mv != nullptr) != (dm != nullptr) || (ov != nullptr) != (doff != nullptr) ||
+        (pv != nullptr) != (dprior != nullptr)) {
+      set_error("requirement failed: m / offset / prior must be given exactly when they were reserved");
+      return SGLM_EINVAL;
+    }
+    if (nr == 0) return SGLM_OK;
+    const double t0 = now_ms();
+    int rc = h2d_block(dX + row0, n_pad, X, ldx, nr, p);
+    for (auto pr : {std::make_pair(dy, yv), std::make_pair(dm, mv), std::make_pair(doff, ov),
+                    std::make_pair(dprior, pv)})
+      if (!rc && pr.second) rc = h2d_block(pr.first + row0, n_pad, pr.second, nr, nr, 1);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    load_ms += now_ms() - t0;
+    const int nvec = 1 + (mv != nullptr) + (ov != nullptr) + (pv != nullptr);
+    load_bytes += (int64_t)sizeof(double) * nr * (p + nvec);
+    rows_loaded += nr;
+    return SGLM_OK;
+  }
+
+  int check_loaded() const {
+    if (p <= 0) {
+      set_error("requirement failed: no data set (sglm_set_data)");
+      return SGLM_EINVAL;
+    }
+    if (!procx.on && rows_loaded < n) {
+      set_error("requirement failed: " + std::to_string(n - rows_loaded) +
+                " reserved rows were never written (sglm_set_rows)");
+      return SGLM_EINVAL;
+    }
+    return SGLM_OK;
+  }
+
+  // ---- scoring of new rows (sglm_predict_new): its own scratch, the shard stays resident ----
+  int predict_new(const double* X, int64_t nn, int64_t pp, int64_t ldx, const double* beta, const double* off,
+                  const double* mv, int family, int link, int type, double* out) {
+    HIPCHK(hipSetDevice(device));
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nn, ((int64_t)1 << 27) / std::max<int64_t>(pp, 1)));
+    if (pp * chunk > xs_cap) {
+      if (dxs) HIPCHK(hipFree(dxs));
+      dxs = nullptr;
+      HIPCHK(hipMalloc(&dxs, sizeof(double) * (size_t)(pp * chunk)));
+      xs_cap = pp * chunk;
+    }
+    if (chunk > vs_cap) {
+      for (double** q : {&dvs, &dms, &dos}) {
+        if (*q) HIPCHK(hipFree(*q));
+        *q = nullptr;
+        HIPCHK(hipMalloc(q, sizeof(double) * (size_t)chunk));
+      }
+      vs_cap = chunk;
+    }
+    int rc = ensure_beta(pp);
+    if (rc) return rc;
+    std::memcpy(hbeta, beta, sizeof(double) * pp);
+    HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * pp, hipMemcpyHostToDevice, st));
+    for (int64_t r0 = 0; r0 < nn; r0 += chunk) {
+      const int64_t nr = std::min(chunk, nn - r0);
+      rc = h2d_block(dxs, nr, X + r0, ldx, nr, pp);
+      if (!rc && off) rc = h2d_block(dos, nr, off + r0, nr, nr, 1);
+      if (!rc && mv) rc = h2d_block(dms, nr, mv + r0, nr, nr, 1);
+      if (rc) return rc;
+      HIPCHK(launch_predict(dxs, nr, (int)pp, nr, dbeta, off ? dos : nullptr, dvs, st, ProcX{}));
+      if (type == SGLM_PREDICT_RESPONSE) HIPCHK(launch_unlink(dvs, mv ? dms : nullptr, nr, family, link, st));
+      HIPCHK(hipMemcpyAsync(out + r0, dvs, sizeof(double) * nr, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    return SGLM_OK;
+  }
+  // hbeta / dbeta hold at least pp doubles (scoring before any shard exists)
+  int ensure_beta(int64_t pp) {
+    if (red_cap >= pp && dbeta) return SGLM_OK;
+    const int64_t need = std::max<int64_t>(pp, red_cap);
+    if (dred) HIPCHK(hipFree(dred));
+    if (dbeta) HIPCHK(hipFree(dbeta));
+    if (hred) HIPCHK(hipHostFree(hred));
+    if (hbeta) HIPCHK(hipHostFree(hbeta));
+    dred = dbeta = hred = hbeta = nullptr;
+    HIPCHK(hipMalloc(&dred, sizeof(double) * need));
+    HIPCHK(hipMalloc(&dbeta, sizeof(double) * need));
+    HIPCHK(hipHostMalloc(&hred, sizeof(double) * need, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&hbeta, sizeof(double) * need, hipHostMallocDefault));
+    red_cap = need;
+    return SGLM_OK;
+  }
+
   // ---- Backend ----
   int global_sums(double* out2) override {
+    if (group()) {  // shard order, as createBinomialDeviance sums partitions (GLM.scala:407)
+      out2[0] = out2[1] = 0.0;
+      for (sglm_engine* s : subs) {
+        double t[2];
+        if (int rc = s->global_sums(t)) return rc;
+        out2[0] += t[0];
+        out2[1] += t[1];
+      }
+      return SGLM_OK;
+    }
     HIPCHK(hipSetDevice(device));
+    if (int rc = check_loaded()) return rc;
     const int nparts = 1024;
     HIPCHK(launch_ysum(dy, n, dpart, nparts, st));
     std::vector<double> h(nparts);
@@ -382,12 +588,50 @@ struct sglm_engine : public Backend {
   }
 
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
-    HIPCHK(hipSetDevice(device));
-    if (p <= 0) {
-      set_error("requirement failed: no data set (sglm_set_data)");
-      return SGLM_EINVAL;
-    }
+    if (group()) return group_pass(mode, beta, mu0, ybar, family, link, packed);
+    int rc = enqueue_pass(mode, beta, mu0, ybar, family, link);
+    if (rc) return rc;
     const int64_t plen = packed_len(p);
+    if (comm_on_device()) {
+      rc = allreduce_device(dred, plen);
+      if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * plen, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    rc = pass_timing();
+    if (rc) return rc;
+    red_on_device = comm_on_device() || comm.kind == 0;
+    if (!comm_on_device()) {
+      rc = allreduce_host(hred, plen);
+      if (rc) return rc;
+    }
+    std::memcpy(packed, hred, sizeof(double) * plen);
+    return SGLM_OK;
+  }
+
+  // Kernel times of the pass just synchronised (HIP events on this engine's stream).
+  int pass_timing() {
+    float k1 = 0.f, k2 = 0.f;
+    HIPCHK(hipEventElapsedTime(&k1, ev0, ev1));
+    HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
+    if (wide) {
+      float km = 0.f;
+      HIPCHK(hipEventElapsedTime(&km, ev0, evm));
+      row_ms += km;
+      gram_ms += k1 - km;
+    }
+    passes += 1;
+    pass_ms += k1;
+    reduce_ms += k2;
+    last_pass_ms = k1;
+    return SGLM_OK;
+  }
+
+  // H2D beta, the pass kernels and the fixed-order partial reduction into dred -- all
+  // asynchronous on this engine's stream (a multi-device handle enqueues every shard first).
+  int enqueue_pass(int mode, const double* beta, double mu0, double ybar, int family, int link) {
+    HIPCHK(hipSetDevice(device));
+    if (int rc = check_loaded()) return rc;
     if (beta) {
       std::memcpy(hbeta, beta, sizeof(double) * p);
       HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * p, hipMemcpyHostToDevice, st));
@@ -467,32 +711,53 @@ struct sglm_engine : public Backend {
       HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st));
     }
     HIPCHK(hipEventRecord(ev2, st));
-    int rc = SGLM_OK;
-    if (comm_on_device()) {
-      rc = allreduce_device(dred, plen);
-      if (rc) return rc;
+    return SGLM_OK;
+  }
+
+  // ---- multi-device handle: every shard's pass enqueued, then one reduction ----
+  // Distinct devices: ncclAllReduce of the packed buffers in one RCCL group call (xGMI), every
+  // shard ends with the sum.  Repeated devices (rehearsal on fewer GPUs): host sums in shard
+  // order.  Either way the wide-path device solver reads shard 0's buffers.
+  int group_pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) {
+    const int64_t plen = packed_len(subs[0]->p);
+    for (sglm_engine* s : subs)
+      if (int rc = s->enqueue_pass(mode, beta, mu0, ybar, family, link)) return rc;
+    const double t0 = now_ms();
+    if (!gcomms.empty()) {
+      ncclResult_t r = ncclGroupStart();
+      for (size_t d = 0; d < subs.size() && r == ncclSuccess; ++d)
+        r = ncclAllReduce(subs[d]->dred, subs[d]->dred, (size_t)plen, ncclFloat64, ncclSum, gcomms[d], subs[d]->st);
+      ncclResult_t r2 = ncclGroupEnd();
+      if (r != ncclSuccess || r2 != ncclSuccess) {
+        set_error(std::string("RCCL ncclAllReduce (group): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+        return SGLM_ECOMM;
+      }
+      sglm_engine* s0 = subs[0];
+      HIPCHK(hipSetDevice(s0->device));
+      HIPCHK(hipMemcpyAsync(s0->hred, s0->dred, sizeof(double) * plen, hipMemcpyDeviceToHost, s0->st));
+      for (sglm_engine* s : subs) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->st));
+        if (int rc = s->pass_timing()) return rc;
+      }
+      std::memcpy(packed, s0->hred, sizeof(double) * plen);
+      s0->red_on_device = true;
+    } else {
+      for (sglm_engine* s : subs) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipMemcpyAsync(s->hred, s->dred, sizeof(double) * plen, hipMemcpyDeviceToHost, s->st));
+      }
+      for (sglm_engine* s : subs) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->st));
+        if (int rc = s->pass_timing()) return rc;
+      }
+      std::memcpy(packed, subs[0]->hred, sizeof(double) * plen);
+      for (size_t d = 1; d < subs.size(); ++d)
+        for (int64_t k = 0; k < plen; ++k) packed[k] += subs[d]->hred[k];
+      subs[0]->red_on_device = false;
     }
-    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * plen, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    float k1 = 0.f, k2 = 0.f;
-    HIPCHK(hipEventElapsedTime(&k1, ev0, ev1));
-    HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
-    if (wide) {
-      float km = 0.f;
-      HIPCHK(hipEventElapsedTime(&km, ev0, evm));
-      row_ms += km;
-      gram_ms += k1 - km;
-    }
-    passes += 1;
-    pass_ms += k1;
-    reduce_ms += k2;
-    last_pass_ms = k1;
-    red_on_device = comm_on_device() || comm.kind == 0;
-    if (!comm_on_device()) {
-      rc = allreduce_host(hred, plen);
-      if (rc) return rc;
-    }
-    std::memcpy(packed, hred, sizeof(double) * plen);
+    comm.ms += now_ms() - t0;
     return SGLM_OK;
   }
 
@@ -513,6 +778,15 @@ struct sglm_engine : public Backend {
   }
 
   int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) override {
+    if (group()) {
+      for (int k = 0; k < NS; ++k) s[k] = 0.0;
+      for (sglm_engine* sub : subs) {
+        double t[NS];
+        if (int rc = sub->stats(mode, beta, mu0, ybar, family, link, t)) return rc;
+        for (int k = 0; k < NS; ++k) s[k] += t[k];
+      }
+      return SGLM_OK;
+    }
     HIPCHK(hipSetDevice(device));
     if (mode == MODE_LM_RESID) {  // pred = X * coefs into the eta buffer
       std::memcpy(hbeta, beta, sizeof(double) * p);
@@ -560,6 +834,7 @@ struct DeviceSolver : public SolverIface {
   double *dA = nullptr, *dB = nullptr, *dAi = nullptr, *dpk = nullptr;
   rocblas_int* dinfo = nullptr;
   std::unique_ptr<HostSolver> host;
+  std::vector<double> ldiag;
   bool on_host = false, have_factor = false;
   DeviceSolver(sglm_engine* eng, int64_t pp) : e(eng), p(pp) {}
   ~DeviceSolver() override {
@@ -595,7 +870,20 @@ struct DeviceSolver : public SolverIface {
     }
     rocblas_int info = 0;
     HIPCHK(hipMemcpyAsync(&info, dinfo, sizeof info, hipMemcpyDeviceToHost, e->st));
+    if (info == 0) {  // diag(L) for the collinearity check (solve.hpp chol_pivot_ratio)
+      ldiag.resize((size_t)p);
+      HIPCHK(hipMemcpy2DAsync(ldiag.data(), sizeof(double), dA, sizeof(double) * (size_t)(p + 1), sizeof(double),
+                              (size_t)p, hipMemcpyDeviceToHost, e->st));
+    }
     HIPCHK(hipStreamSynchronize(e->st));
+    if (info == 0) {
+      double r = 1.0;
+      for (int64_t j = 0; j < p; ++j) {
+        const double a = packed[j * (j + 1) / 2 + j];
+        if (a > 0.0) r = std::fmin(r, ldiag[(size_t)j] * ldiag[(size_t)j] / a);
+      }
+      if (r < LU_SWITCH_RATIO) info = -1;  // ill-conditioned: the reference's LU inverse on the host
+    }
     if (info != 0) {
       on_host = true;
       have_factor = false;
@@ -654,6 +942,7 @@ struct DeviceSolver : public SolverIface {
 }  // namespace
 
 std::unique_ptr<SolverIface> sglm_engine::make_solver(int64_t pp) {
+  if (group()) return subs[0]->make_solver(pp);
   if (wide) return std::make_unique<DeviceSolver>(this, pp);
   return std::make_unique<HostSolver>(pp);
 }
@@ -779,74 +1068,195 @@ int sglm_create(int device, sglm_engine** out) {
 
 void sglm_destroy(sglm_engine* h) { delete h; }
 
-static int set_data_impl(sglm_engine* h, const double* X, int64_t n, int64_t p, int64_t ldx, const double* y,
-                         const double* m, const double* off, const double* prior, hipMemcpyKind kind) {
+int sglm_create_multi(const int* devs, int ndev, sglm_engine** out) {
+  if (!out || !devs || ndev < 1) {
+    set_error("requirement failed: devs[ndev], ndev >= 1, out handle pointer");
+    return SGLM_EINVAL;
+  }
+  *out = nullptr;
+  auto* g = new sglm_engine();
+  g->device = devs[0];
+  for (int d = 0; d < ndev; ++d) {
+    sglm_engine* s = nullptr;
+    int rc = sglm_create(devs[d], &s);
+    if (rc) {
+      delete g;
+      return rc;
+    }
+    g->subs.push_back(s);
+  }
+  bool distinct = true;
+  for (int a = 0; a < ndev; ++a)
+    for (int b = 0; b < a; ++b) distinct = distinct && devs[a] != devs[b];
+  if (distinct) {  // one communicator per device, one process (ncclCommInitAll)
+    g->gcomms.assign((size_t)ndev, nullptr);
+    ncclResult_t r = ncclCommInitAll(g->gcomms.data(), ndev, devs);
+    if (r != ncclSuccess) {
+      g->gcomms.clear();
+      set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+      delete g;
+      return SGLM_ECOMM;
+    }
+  }
+  *out = g;
+  return SGLM_OK;
+}
+
+int sglm_handle_devices(sglm_engine* h, int* ndev) {
+  if (int rc = check_handle(h)) return rc;
+  *ndev = h->group() ? (int)h->subs.size() : 1;
+  return SGLM_OK;
+}
+
+// Row ranges of a multi-device handle's shards: Spark's slicing [d n / D, (d+1) n / D).
+static void group_split(sglm_engine* h, int64_t n) {
+  const int64_t D = (int64_t)h->subs.size();
+  h->sub_lo.assign((size_t)D + 1, 0);
+  for (int64_t d = 0; d <= D; ++d) h->sub_lo[(size_t)d] = (int64_t)((__int128)d * n / D);
+  h->g_n = n;
+}
+
+static int reserve_impl(sglm_engine* h, int64_t n, int64_t p, int has_m, int has_off, int has_prior) {
+  if (n <= 0 || p <= 0) {
+    set_error("requirement failed: n >= 1, p >= 1");
+    return SGLM_EINVAL;
+  }
+  if (h->group()) {
+    if (n < (int64_t)h->subs.size()) {
+      set_error("requirement failed: at least one row per device");
+      return SGLM_EINVAL;
+    }
+    group_split(h, n);
+    for (size_t d = 0; d < h->subs.size(); ++d)
+      if (int rc = reserve_impl(h->subs[d], h->sub_lo[d + 1] - h->sub_lo[d], p, has_m, has_off, has_prior)) return rc;
+    return SGLM_OK;
+  }
+  return h->alloc_data(n, p, has_m != 0, has_off != 0, has_prior != 0);
+}
+
+int sglm_reserve(sglm_engine* h, int64_t n, int64_t p, int has_m, int has_offset, int has_prior) {
+  if (int rc = check_handle(h)) return rc;
+  return reserve_impl(h, n, p, has_m, has_offset, has_prior);
+}
+
+static int set_rows_impl(sglm_engine* h, int64_t row0, int64_t nr, const double* X, int64_t ldx, const double* y,
+                         const double* m, const double* off, const double* prior) {
+  if (!h->group()) return h->set_rows(row0, nr, X, ldx, y, m, off, prior);
+  if (h->g_n <= 0 || row0 < 0 || nr < 0 || row0 + nr > h->g_n) {
+    set_error("requirement failed: sglm_reserve first; 0 <= row0, row0 + nrows <= reserved rows");
+    return SGLM_EINVAL;
+  }
+  for (size_t d = 0; d < h->subs.size(); ++d) {  // the block's intersection with each shard
+    const int64_t a = std::max(row0, h->sub_lo[d]), b = std::min(row0 + nr, h->sub_lo[d + 1]);
+    if (a >= b) continue;
+    const int64_t o = a - row0;
+    auto sh = [&](const double* v) { return v ? v + o : nullptr; };
+    if (int rc = h->subs[d]->set_rows(a - h->sub_lo[d], b - a, X + o, ldx, sh(y), sh(m), sh(off), sh(prior)))
+      return rc;
+  }
+  return SGLM_OK;
+}
+
+int sglm_set_rows(sglm_engine* h, int64_t row0, int64_t nrows, const double* X, int64_t ldx, const double* y,
+                  const double* m, const double* offset, const double* prior) {
+  if (int rc = check_handle(h)) return rc;
+  return set_rows_impl(h, row0, nrows, X, ldx, y, m, offset, prior);
+}
+
+int sglm_set_data(sglm_engine* h, const double* X, int64_t n, int64_t p, int64_t ldx, const double* y,
+                  const double* m, const double* offset, const double* prior) {
   if (int rc = check_handle(h)) return rc;
   if (!X || !y || ldx < n || n <= 0 || p <= 0) {
     set_error("requirement failed: X, y non-null, n >= 1, p >= 1, ldx >= n");
     return SGLM_EINVAL;
   }
-  int rc = h->alloc_data(n, p, m != nullptr, off != nullptr, prior != nullptr);
+  int rc = reserve_impl(h, n, p, m != nullptr, offset != nullptr, prior != nullptr);
   if (rc) return rc;
-  const size_t vb = sizeof(double) * (size_t)n;
-  HIPCHK(hipMemcpy2DAsync(h->dX, sizeof(double) * h->n_pad, X, sizeof(double) * ldx, vb, (size_t)p, kind, h->st));
-  HIPCHK(hipMemcpyAsync(h->dy, y, vb, kind, h->st));
-  if (m) HIPCHK(hipMemcpyAsync(h->dm, m, vb, kind, h->st));
-  if (off) HIPCHK(hipMemcpyAsync(h->doff, off, vb, kind, h->st));
-  if (prior) HIPCHK(hipMemcpyAsync(h->dprior, prior, vb, kind, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  return SGLM_OK;
-}
-
-int sglm_set_data(sglm_engine* h, const double* X, int64_t n, int64_t p, int64_t ldx, const double* y,
-                  const double* m, const double* offset, const double* prior) {
-  return set_data_impl(h, X, n, p, ldx, y, m, offset, prior, hipMemcpyHostToDevice);
+  return set_rows_impl(h, 0, n, X, ldx, y, m, offset, prior);
 }
 
 int sglm_set_data_device(sglm_engine* h, const double* dX, int64_t n, int64_t p, int64_t ldx, const double* dy,
                          const double* dm, const double* doffset, const double* dprior) {
-  return set_data_impl(h, dX, n, p, ldx, dy, dm, doffset, dprior, hipMemcpyDeviceToDevice);
+  if (int rc = check_handle(h)) return rc;
+  if (h->group()) {
+    set_error("requirement failed: sglm_set_data_device takes one device's memory; use a single-device handle");
+    return SGLM_EINVAL;
+  }
+  if (!dX || !dy || ldx < n || n <= 0 || p <= 0) {
+    set_error("requirement failed: X, y non-null, n >= 1, p >= 1, ldx >= n");
+    return SGLM_EINVAL;
+  }
+  int rc = h->alloc_data(n, p, dm != nullptr, doffset != nullptr, dprior != nullptr);
+  if (rc) return rc;
+  const size_t vb = sizeof(double) * (size_t)n;
+  const hipMemcpyKind kind = hipMemcpyDeviceToDevice;
+  HIPCHK(hipMemcpy2DAsync(h->dX, sizeof(double) * h->n_pad, dX, sizeof(double) * ldx, vb, (size_t)p, kind, h->st));
+  HIPCHK(hipMemcpyAsync(h->dy, dy, vb, kind, h->st));
+  if (dm) HIPCHK(hipMemcpyAsync(h->dm, dm, vb, kind, h->st));
+  if (doffset) HIPCHK(hipMemcpyAsync(h->doff, doffset, vb, kind, h->st));
+  if (dprior) HIPCHK(hipMemcpyAsync(h->dprior, dprior, vb, kind, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->rows_loaded = n;
+  return SGLM_OK;
+}
+
+static int synth_impl(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, bool proc) {
+  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
+    set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
+    return SGLM_EINVAL;
+  }
+  if (h->group()) {
+    if (n < (int64_t)h->subs.size()) {
+      set_error("requirement failed: at least one row per device");
+      return SGLM_EINVAL;
+    }
+    group_split(h, n);
+    for (size_t d = 0; d < h->subs.size(); ++d)
+      if (int rc = synth_impl(h->subs[d], kind, row0 + h->sub_lo[d], h->sub_lo[d + 1] - h->sub_lo[d], p, seed, proc))
+        return rc;
+    return SGLM_OK;
+  }
+  int rc = h->alloc_data(n, p, false, kind == 2, kind == 2, proc);
+  if (rc) return rc;
+  const double scale = 1.0 / std::sqrt((double)p);
+  // procedural: y (and offset / prior) from the same generator; X itself is not stored
+  HIPCHK(launch_synth(kind, row0, n, (int)p, seed, scale, proc ? nullptr : h->dX, h->n_pad, h->dy, nullptr, h->doff,
+                      h->dprior, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->rows_loaded = n;
+  if (proc) {
+    h->procx.on = 1;
+    h->procx.kind = kind;
+    h->procx.p = (int)p;
+    h->procx.row0 = row0;
+    h->procx.n = n;
+    h->procx.kx = splitmix64_host(seed);
+    h->procx.scale = scale;
+  }
+  return SGLM_OK;
 }
 
 int sglm_synth(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed) {
   if (int rc = check_handle(h)) return rc;
-  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
-    set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
-    return SGLM_EINVAL;
-  }
-  int rc = h->alloc_data(n, p, false, kind == 2, kind == 2);
-  if (rc) return rc;
-  const double scale = 1.0 / std::sqrt((double)p);
-  HIPCHK(launch_synth(kind, row0, n, (int)p, seed, scale, h->dX, h->n_pad, h->dy, nullptr, h->doff, h->dprior, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  return SGLM_OK;
+  return synth_impl(h, kind, row0, n, p, seed, false);
 }
 
 int sglm_synth_procedural(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed) {
   if (int rc = check_handle(h)) return rc;
-  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
-    set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
-    return SGLM_EINVAL;
-  }
-  int rc = h->alloc_data(n, p, false, kind == 2, kind == 2, true);
-  if (rc) return rc;
-  const double scale = 1.0 / std::sqrt((double)p);
-  // y (and offset / prior) from the same generator; X itself is not stored
-  HIPCHK(launch_synth(kind, row0, n, (int)p, seed, scale, nullptr, h->n_pad, h->dy, nullptr, h->doff, h->dprior,
-                      h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  h->procx.on = 1;
-  h->procx.kind = kind;
-  h->procx.p = (int)p;
-  h->procx.row0 = row0;
-  h->procx.n = n;
-  h->procx.kx = splitmix64_host(seed);
-  h->procx.scale = scale;
-  return SGLM_OK;
+  return synth_impl(h, kind, row0, n, p, seed, true);
 }
 
-int sglm_get_data(sglm_engine* h, double* X, double* y, double* m, double* offset, double* prior) {
-  if (int rc = check_handle(h)) return rc;
+static int get_data_impl(sglm_engine* h, double* X, int64_t ldx, double* y, double* m, double* offset,
+                         double* prior) {
+  if (h->group()) {
+    for (size_t d = 0; d < h->subs.size(); ++d) {
+      const int64_t o = h->sub_lo[d];
+      auto sh = [&](double* v) { return v ? v + o : nullptr; };
+      if (int rc = get_data_impl(h->subs[d], X ? X + o : nullptr, ldx, sh(y), sh(m), sh(offset), sh(prior)))
+        return rc;
+    }
+    return SGLM_OK;
+  }
   if (X && h->procx.on) {
     set_error("requirement failed: a procedural shard stores no X");
     return SGLM_EINVAL;
@@ -854,7 +1264,8 @@ int sglm_get_data(sglm_engine* h, double* X, double* y, double* m, double* offse
   HIPCHK(hipSetDevice(h->device));
   const size_t vb = sizeof(double) * (size_t)h->n;
   if (X)
-    HIPCHK(hipMemcpy2DAsync(X, vb, h->dX, sizeof(double) * h->n_pad, vb, (size_t)h->p, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpy2DAsync(X, sizeof(double) * (size_t)ldx, h->dX, sizeof(double) * h->n_pad, vb, (size_t)h->p,
+                            hipMemcpyDeviceToHost, h->st));
   if (y) HIPCHK(hipMemcpyAsync(y, h->dy, vb, hipMemcpyDeviceToHost, h->st));
   if (m && h->dm) HIPCHK(hipMemcpyAsync(m, h->dm, vb, hipMemcpyDeviceToHost, h->st));
   if (offset && h->doff) HIPCHK(hipMemcpyAsync(offset, h->doff, vb, hipMemcpyDeviceToHost, h->st));
@@ -863,8 +1274,21 @@ int sglm_get_data(sglm_engine* h, double* X, double* y, double* m, double* offse
   return SGLM_OK;
 }
 
+int sglm_get_data(sglm_engine* h, double* X, double* y, double* m, double* offset, double* prior) {
+  if (int rc = check_handle(h)) return rc;
+  return get_data_impl(h, X, h->group() ? h->g_n : h->n, y, m, offset, prior);
+}
+
+static int no_group(sglm_engine* h, const char* what) {
+  if (!h->group()) return SGLM_OK;
+  set_error(std::string("requirement failed: ") + what +
+            " joins one device to other processes; a multi-device handle already reduces over its devices");
+  return SGLM_EINVAL;
+}
+
 int sglm_set_comm(sglm_engine* h, sglm_allreduce_fn fn, void* ctx, int on_device) {
   if (int rc = check_handle(h)) return rc;
+  if (int rc = no_group(h, "sglm_set_comm")) return rc;
   h->comm.kind = fn ? 1 : 0;
   h->comm.fn = fn;
   h->comm.ctx = ctx;
@@ -905,6 +1329,7 @@ int sglm_rccl_unique_id(void* out128) {
 
 int sglm_set_comm_rccl(sglm_engine* h, int nranks, int rank, const void* unique_id128) {
   if (int rc = check_handle(h)) return rc;
+  if (int rc = no_group(h, "sglm_set_comm_rccl")) return rc;
   if (nranks < 1 || rank < 0 || rank >= nranks || !unique_id128) {
     set_error("requirement failed: 0 <= rank < nranks, unique id");
     return SGLM_EINVAL;
@@ -925,16 +1350,23 @@ int sglm_set_comm_rccl(sglm_engine* h, int nranks, int rank, const void* unique_
   return SGLM_OK;
 }
 
+// The handle holds a complete design: every reserved row written (or generated).
+static int check_ready(sglm_engine* h) {
+  if (h->group()) {
+    for (sglm_engine* s : h->subs)
+      if (int rc = s->check_loaded()) return rc;
+    return SGLM_OK;
+  }
+  return h->check_loaded();
+}
+
 int sglm_fit_glm(sglm_engine* h, const sglm_glm_opts* opts, sglm_preglm* out) {
   if (int rc = check_handle(h)) return rc;
   if (!opts || !out || !out->coefs || !out->std_err) {
     set_error("requirement failed: opts, out, out->coefs, out->std_err");
     return SGLM_EINVAL;
   }
-  if (h->p <= 0) {
-    set_error("requirement failed: no data set (sglm_set_data)");
-    return SGLM_EINVAL;
-  }
+  if (int rc = check_ready(h)) return rc;
   return glm_drive(*h, *opts, out);
 }
 
@@ -944,10 +1376,7 @@ int sglm_fit_lm(sglm_engine* h, sglm_prelm* out) {
     set_error("requirement failed: out, out->coefs, out->std_err");
     return SGLM_EINVAL;
   }
-  if (h->p <= 0) {
-    set_error("requirement failed: no data set (sglm_set_data)");
-    return SGLM_EINVAL;
-  }
+  if (int rc = check_ready(h)) return rc;
   return lm_drive(*h, out);
 }
 
@@ -958,7 +1387,8 @@ int sglm_irls_pass(sglm_engine* h, const sglm_glm_opts* opts, const double* beta
     set_error("requirement failed: opts with a supported family/link");
     return SGLM_EINVAL;
   }
-  const int64_t p = h->p;
+  if (int rc = check_ready(h)) return rc;
+  const int64_t p = h->ncols();
   std::vector<double> packed((size_t)packed_len(p)), g((size_t)(p * p)), x((size_t)p);
   const int mode = beta ? MODE_IRLS : (opts->init_mode == SGLM_INIT_MULTIPLE ? MODE_INIT_MULTI : MODE_INIT_SINGLE);
   int rc = h->pass(mode, beta, mu0, 0.0, opts->family, opts->link, packed.data());
@@ -976,7 +1406,29 @@ int sglm_irls_iterations(sglm_engine* h, const sglm_glm_opts* opts, double* beta
     set_error("requirement failed: opts, beta, iters >= 0");
     return SGLM_EINVAL;
   }
+  if (int rc = check_ready(h)) return rc;
   return irls_iterate(*h, *opts, beta, iters, last_dev);
+}
+
+// eta (+ offset) of the resident rows -- or, type SGLM_PREDICT_RESPONSE, mu = unlink(eta, m) --
+// into out [n_local]; a multi-device handle concatenates its shards in row order.
+static int predict_resident(sglm_engine* h, const double* beta, int add_offset, int family, int link, int type,
+                            double* out) {
+  if (h->group()) {
+    for (size_t d = 0; d < h->subs.size(); ++d)
+      if (int rc = predict_resident(h->subs[d], beta, add_offset, family, link, type, out + h->sub_lo[d])) return rc;
+    return SGLM_OK;
+  }
+  if (int rc = h->check_loaded()) return rc;
+  HIPCHK(hipSetDevice(h->device));
+  std::memcpy(h->hbeta, beta, sizeof(double) * h->p);
+  HIPCHK(hipMemcpyAsync(h->dbeta, h->hbeta, sizeof(double) * h->p, hipMemcpyHostToDevice, h->st));
+  HIPCHK(launch_predict(h->dX, h->n_pad, (int)h->p, h->n, h->dbeta, add_offset ? h->doff : nullptr, h->deta, h->st,
+                        h->procx));
+  if (type == SGLM_PREDICT_RESPONSE) HIPCHK(launch_unlink(h->deta, h->dm, h->n, family, link, h->st));
+  HIPCHK(hipMemcpyAsync(out, h->deta, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return SGLM_OK;
 }
 
 int sglm_predict(sglm_engine* h, const double* beta, int add_offset, double* out) {
@@ -985,18 +1437,55 @@ int sglm_predict(sglm_engine* h, const double* beta, int add_offset, double* out
     set_error("requirement failed: beta, out");
     return SGLM_EINVAL;
   }
-  HIPCHK(hipSetDevice(h->device));
-  std::memcpy(h->hbeta, beta, sizeof(double) * h->p);
-  HIPCHK(hipMemcpyAsync(h->dbeta, h->hbeta, sizeof(double) * h->p, hipMemcpyHostToDevice, h->st));
-  HIPCHK(launch_predict(h->dX, h->n_pad, (int)h->p, h->n, h->dbeta, add_offset ? h->doff : nullptr, h->deta, h->st,
-                        h->procx));
-  HIPCHK(hipMemcpyAsync(out, h->deta, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  return SGLM_OK;
+  return predict_resident(h, beta, add_offset, FAM_GAUSSIAN, LNK_IDENTITY, SGLM_PREDICT_LINK, out);
+}
+
+int sglm_predict_glm(sglm_engine* h, const double* beta, int family, int link, int type, int add_offset,
+                     double* out) {
+  if (int rc = check_handle(h)) return rc;
+  if (!beta || !out || !family_link_valid(family, link) || (type != SGLM_PREDICT_LINK && type != SGLM_PREDICT_RESPONSE)) {
+    set_error("requirement failed: beta, out, a supported family/link, type link or response");
+    return SGLM_EINVAL;
+  }
+  return predict_resident(h, beta, add_offset, family, link, type, out);
+}
+
+int sglm_predict_new(sglm_engine* h, const double* X, int64_t n, int64_t p, int64_t ldx, const double* beta,
+                     const double* offset, const double* m, int family, int link, int type, double* out) {
+  if (int rc = check_handle(h)) return rc;
+  if (!X || !beta || !out || n < 0 || p <= 0 || ldx < n || !family_link_valid(family, link) ||
+      (type != SGLM_PREDICT_LINK && type != SGLM_PREDICT_RESPONSE)) {
+    set_error("requirement failed: X, beta, out, n >= 0, p >= 1, ldx >= n, a supported family/link, type link "
+              "or response");
+    return SGLM_EINVAL;
+  }
+  if (n == 0) return SGLM_OK;
+  sglm_engine* e = h->group() ? h->subs[0] : h;  // new rows are scored on the first device
+  return e->predict_new(X, n, p, ldx, beta, offset, m, family, link, type, out);
 }
 
 int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   if (int rc = check_handle(h)) return rc;
+  if (h->group()) {  // kernel times: the slowest shard; rows and bytes: all shards
+    if (int rc = sglm_get_stats(h->subs[0], out)) return rc;
+    for (size_t d = 1; d < h->subs.size(); ++d) {
+      sglm_stats s{};
+      (void)sglm_get_stats(h->subs[d], &s);
+      out->pass_kernel_ms = std::max(out->pass_kernel_ms, s.pass_kernel_ms);
+      out->reduce_kernel_ms = std::max(out->reduce_kernel_ms, s.reduce_kernel_ms);
+      out->last_pass_ms = std::max(out->last_pass_ms, s.last_pass_ms);
+      out->row_kernel_ms = std::max(out->row_kernel_ms, s.row_kernel_ms);
+      out->gram_kernel_ms = std::max(out->gram_kernel_ms, s.gram_kernel_ms);
+      out->n_local += s.n_local;
+      out->load_ms += s.load_ms;
+      out->load_bytes += s.load_bytes;
+    }
+    out->comm_ms = h->comm.ms;
+    out->solve_ms = h->solve_ms;
+    out->ndev = (int)h->subs.size();
+    out->rccl_group = h->gcomms.empty() ? 0 : 1;
+    return SGLM_OK;
+  }
   out->passes = h->passes;
   out->pass_kernel_ms = h->pass_ms;
   out->reduce_kernel_ms = h->reduce_ms;
@@ -1011,15 +1500,22 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->wide_panels = h->wide ? h->npan : 0;
   out->row_kernel_ms = h->row_ms;
   out->gram_kernel_ms = h->wide ? h->gram_ms : h->pass_ms;
+  out->load_ms = h->load_ms;
+  out->load_bytes = h->load_bytes;
+  out->ndev = 1;
+  out->rccl_group = 0;
   return SGLM_OK;
 }
 
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
+  for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
   h->passes = 0;
   h->pass_ms = h->reduce_ms = h->last_pass_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;
+  h->load_ms = 0.0;
+  h->load_bytes = 0;
   return SGLM_OK;
 }
 
@@ -1042,6 +1538,77 @@ int sglm_fit_lm_external(const sglm_backend* be, sglm_allreduce_fn fn, void* com
   double sums[2];
   if (int rc = eb.global_sums(sums)) return rc;  // establishes the rank count
   return lm_drive(eb, out);
+}
+
+// ---- in-process communicator: N host threads, one handle each (a JVM driver's thread pool) ----
+// Every rank's call blocks until all N have arrived; the last to arrive sums the N buffers in
+// rank order (deterministic, independent of arrival order) and writes the sum into all of them.
+struct sglm_local_comm {
+  int nranks = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<double*> bufs;
+  int64_t count = -1;
+  bool failed = false;  // this round: a rank passed another count
+  bool result = false;  // the last completed round failed (read by its waiters only)
+  struct Rank {
+    sglm_local_comm* c;
+    int rank;
+  };
+  std::vector<Rank> ranks;
+};
+
+int sglm_local_comm_create(int nranks, sglm_local_comm** out) {
+  if (!out || nranks < 1) {
+    set_error("requirement failed: nranks >= 1, out");
+    return SGLM_EINVAL;
+  }
+  auto* c = new sglm_local_comm();
+  c->nranks = nranks;
+  c->bufs.assign((size_t)nranks, nullptr);
+  for (int r = 0; r < nranks; ++r) c->ranks.push_back({c, r});
+  *out = c;
+  return SGLM_OK;
+}
+
+void sglm_local_comm_destroy(sglm_local_comm* c) { delete c; }
+
+void* sglm_local_comm_rank(sglm_local_comm* c, int rank) {
+  if (!c || rank < 0 || rank >= c->nranks) return nullptr;
+  return &c->ranks[(size_t)rank];
+}
+
+int sglm_local_allreduce(void* ctx, double* buf, int64_t count, void* stream, int on_device) {
+  (void)stream;
+  auto* rk = static_cast<sglm_local_comm::Rank*>(ctx);
+  if (!rk || on_device) return 1;  // host buffers only
+  sglm_local_comm* c = rk->c;
+  std::unique_lock<std::mutex> lk(c->mu);
+  const uint64_t gen = c->generation;
+  if (c->arrived == 0) {
+    c->count = count;
+    c->failed = false;
+  } else if (count != c->count) {
+    c->failed = true;
+  }
+  c->bufs[(size_t)rk->rank] = buf;
+  if (++c->arrived == c->nranks) {
+    if (!c->failed) {
+      std::vector<double> sum(c->bufs[0], c->bufs[0] + count);
+      for (int r = 1; r < c->nranks; ++r)
+        for (int64_t k = 0; k < count; ++k) sum[(size_t)k] += c->bufs[(size_t)r][k];
+      for (int r = 0; r < c->nranks; ++r) std::memcpy(c->bufs[(size_t)r], sum.data(), sizeof(double) * count);
+    }
+    c->result = c->failed;
+    c->arrived = 0;
+    ++c->generation;
+    c->cv.notify_all();
+  } else {
+    c->cv.wait(lk, [&] { return c->generation != gen; });
+  }
+  return c->result ? 1 : 0;
 }
 
 }  // extern "C"

@@ -521,6 +521,14 @@ __global__ void predict_kernel(const double* __restrict__ X, int64_t ld, int p, 
   }
 }
 
+// mu = unlink(eta, m) in place: muCreate (GLM.scala:334-355) / R's family linkinv, the
+// response-scale prediction.  One instantiation per family/link.
+template <int FAM, int LNK>
+__global__ void unlink_kernel(double* __restrict__ v, const double* __restrict__ m, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = unlink_fn(FAM, LNK, v[i], m ? m[i] : 1.0);
+}
+
 // Block partial sums of y (GLM.scala:420-423 ySums) -- fixed order per block.
 __global__ void ysum_kernel(const double* __restrict__ y, int64_t n, double* __restrict__ part) {
   __shared__ double red[4];
@@ -704,6 +712,28 @@ hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const d
   if (blocks > 65536) blocks = 65536;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, ld, p, n, beta, off, out, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_unlink(double* v, const double* m, int64_t n, int family, int link, hipStream_t st) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  const dim3 g((unsigned)blocks), b(256);
+  if (family == FAM_BINOMIAL && link == LNK_LOGIT)
+    hipLaunchKernelGGL((unlink_kernel<FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, v, m, n);
+  else if (family == FAM_BINOMIAL && link == LNK_PROBIT)
+    hipLaunchKernelGGL((unlink_kernel<FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, v, m, n);
+  else if (family == FAM_BINOMIAL && link == LNK_CLOGLOG)
+    hipLaunchKernelGGL((unlink_kernel<FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, v, m, n);
+  else if (family == FAM_GAUSSIAN)
+    return hipSuccess;  // identity
+  else if (family == FAM_POISSON)
+    hipLaunchKernelGGL((unlink_kernel<FAM_POISSON, LNK_LOG>), g, b, 0, st, v, m, n);
+  else if (family == FAM_GAMMA)
+    hipLaunchKernelGGL((unlink_kernel<FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, v, m, n);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st);
 hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
                           double* out, hipStream_t st, const ProcX& g);
+hipError_t launch_unlink(double* v, const double* m, int64_t n, int family, int link, hipStream_t st);
 hipError_t launch_ysum(const double* y, int64_t n, double* part, int nparts, hipStream_t st);
 uint64_t splitmix64_host(uint64_t x);
 hipError_t launch_synth(int kind, int64_t row0, int64_t n, int p, uint64_t seed, double scale, double* X, int64_t ld,

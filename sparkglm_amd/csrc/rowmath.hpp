@@ -187,7 +187,9 @@ __device__ __noinline__ RowWZ pass_row_ref(int fam, int lnk, int mode, double et
   r.w = pw * (1.0 / (v * (g * g)));
   const double z = (eta + ((y + (-1.0 * mu)) * g)) + (-1.0 * off);
   r.wz = r.w * z;
-  r.dev = unit_dev(fam, y, mu, m, pw);
+  // fitMultipleBinomial re-derives mu = unlink(link(ybar)) only inside zwCreateBinomial; its
+  // null deviance is taken at mu0 = ybar itself (GLM.scala:424-444)
+  r.dev = unit_dev(fam, y, mode == MODE_IRLS ? mu : mu0, m, pw);
   return r;
 }
 
@@ -271,13 +273,9 @@ __device__ __noinline__ RowAcc stats_row_ref(int fam, int lnk, int mode, double 
   RowAcc acc;
 #pragma unroll
   for (int k = 0; k < NS; ++k) acc.s[k] = 0.0;
-  double mu;
-  if (mode == MODE_IRLS) {
-    mu = unlink_fn(fam, lnk, eta, m);
-  } else {
-    const double e0 = link_fn(fam, lnk, mu0, m);
-    mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, e0, m);
-  }
+  // init modes (a fit that stops before its first solve): the statistics at mu0 itself, as
+  // pearsonCalc / llBinomial see the broadcast ybar (GLM.scala:424-426, 465-466)
+  const double mu = (mode == MODE_IRLS) ? unlink_fn(fam, lnk, eta, m) : mu0;
   const double v = variance_fn(fam, mu, m);
   const double r = y + (-1.0 * mu);
   acc.s[S_DEV] += unit_dev(fam, y, mu, m, pw);

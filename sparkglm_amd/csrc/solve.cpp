@@ -4,10 +4,12 @@
 // (utils.scala:103-105, 134-136; LM.scala:197-199, 225-227).  X'WX is symmetric positive
 // definite whenever every working weight is positive, so the engine factors it with
 // Cholesky (half the flops of LU, no pivot search) and keeps the factor of the last solve
-// for the standard errors; a matrix Cholesky rejects (negative weights from the
-// reference's unguarded formulas, or numerical indefiniteness) falls back to LU with
-// partial pivoting, and an exactly singular one is reported like Breeze's
-// MatrixSingularException.
+// for the standard errors.  Two cases take the reference's own algorithm, LU with partial
+// pivoting and the explicit inverse: a matrix Cholesky rejects (negative weights from the
+// reference's unguarded formulas, or numerical indefiniteness), and an ill-conditioned one
+// (chol_pivot_ratio < LU_SWITCH_RATIO, cond >~ 1e6), where the two algorithms' rounding
+// parts by cond * eps -- past the 1e-9 parity bar at cond ~1e7 (tests/test_host_paths.py).
+// An exactly singular matrix is reported like Breeze's MatrixSingularException.
 #include "solve.hpp"
 
 #include <cmath>
@@ -142,10 +144,19 @@ int lu_inverse(double* A, int64_t p) {
   return 0;
 }
 
+double chol_pivot_ratio(const double* L, const double* A, int64_t p) {
+  double r = 1.0;
+  for (int64_t j = 0; j < p; ++j) {
+    const double l = L[j + j * p], a = A[j + j * p];
+    if (a > 0.0) r = std::fmin(r, (l * l) / a);
+  }
+  return r;
+}
+
 int Solver::solve(const double* A, const double* b, double* x) {
   const size_t pp = (size_t)(p_ * p_);
   fac_.assign(A, A + pp);
-  if (chol_factor(fac_.data(), p_) == 0) {
+  if (chol_factor(fac_.data(), p_) == 0 && chol_pivot_ratio(fac_.data(), A, p_) >= LU_SWITCH_RATIO) {
     kind_ = 1;
     chol_solve(fac_.data(), p_, b, x);
     return 0;

@@ -51,6 +51,44 @@ def torch_allreduce(group=None):
     return fn
 
 
+class LocalComm:
+    """The library's in-process communicator (sglm_local_comm): N host threads in one process,
+    one handle (or external fit) each -- the thread-pool alternative to sglm_create_multi.  The
+    sum runs in rank order inside the library, so every rank gets bitwise the same buffer."""
+
+    def __init__(self, nranks: int):
+        self._lib = L.load()
+        c = C.c_void_p()
+        L.check(self._lib.sglm_local_comm_create(int(nranks), C.byref(c)), "sglm_local_comm_create")
+        self._c = c
+        self.nranks = nranks
+        # the C function itself (no Python frame on the reduction path)
+        self.fn = L.ALLREDUCE_FN(C.cast(self._lib.sglm_local_allreduce, C.c_void_p).value)
+
+    def rank(self, r: int) -> "LocalRank":
+        ctx = self._lib.sglm_local_comm_rank(self._c, int(r))
+        if not ctx:
+            raise L.IllegalArgumentException(f"requirement failed: rank {r} of {self.nranks}")
+        return LocalRank(self, ctx)
+
+    def close(self):
+        if getattr(self, "_c", None):
+            self._lib.sglm_local_comm_destroy(self._c)
+            self._c = None
+
+
+class LocalRank:
+    def __init__(self, comm: LocalComm, ctx: int):
+        self.comm, self.ctx = comm, ctx
+
+
+def _comm_args(allreduce):
+    """(C all-reduce function, its context) for a Python callable, a LocalRank, or None."""
+    if isinstance(allreduce, LocalRank):
+        return allreduce.comm.fn, C.c_void_p(allreduce.ctx)
+    return _allreduce_cb(allreduce), None
+
+
 def _allreduce_cb(fn):
     if fn is None:
         return L.ALLREDUCE_FN(lambda ctx, buf, count, stream, dev: 0)
@@ -74,6 +112,7 @@ class _ExternalBackend:
 
     def __init__(self, p: int, local_sums, partials):
         self.p = p
+        self.packed_len = p * (p + 1) // 2 + p + L.NS
 
         def _sums(ctx, out):
             try:
@@ -88,7 +127,10 @@ class _ExternalBackend:
         def _pass(ctx, mode, beta, mu0, ybar, packed):
             try:
                 b = None if not beta else np.ctypeslib.as_array(beta, shape=(p,)).copy()
-                res = np.asarray(partials(int(mode), b, float(mu0), float(ybar)), dtype=np.float64)
+                res = np.ascontiguousarray(partials(int(mode), b, float(mu0), float(ybar)), dtype=np.float64)
+                if res.size != self.packed_len:  # the C side owns exactly packed_len doubles
+                    raise ValueError(f"partials() returned {res.size} doubles, the packed wire format of "
+                                     f"p = {p} holds {self.packed_len}")
                 C.memmove(packed, res.ctypes.data, res.nbytes)
                 return 0
             except Exception:
@@ -104,11 +146,11 @@ def fit_glm_external(p, local_sums, partials, allreduce=None, family="binomial",
                      max_iter=0, init="single", npart=0, max_trace=512) -> FitGLM:
     lib = L.load()
     be = _ExternalBackend(p, local_sums, partials)
-    cb = _allreduce_cb(allreduce)
+    cb, ctx = _comm_args(allreduce)
     o = glm_opts(family, link, tol, False, max_iter, init, npart)
     coefs, se, trace = np.zeros(p), np.zeros(p), np.full(max_trace, np.nan)
     pre = L.PreGLM(L.ptr(coefs), L.ptr(se), 0, 0, 0, 0, 0, 0, 0, L.ptr(trace), max_trace)
-    L.check(lib.sglm_fit_glm_external(C.byref(be.struct), cb, None, C.byref(o), C.byref(pre)),
+    L.check(lib.sglm_fit_glm_external(C.byref(be.struct), cb, ctx, C.byref(o), C.byref(pre)),
             "sglm_fit_glm_external")
     return FitGLM(coefs, se, pre.deviance, pre.null_deviance, pre.pearson, pre.loglik, pre.iter, pre.nrow,
                   pre.npart, trace[: pre.iter + 1].copy())
@@ -117,8 +159,8 @@ def fit_glm_external(p, local_sums, partials, allreduce=None, family="binomial",
 def fit_lm_external(p, local_sums, partials, allreduce=None) -> FitLM:
     lib = L.load()
     be = _ExternalBackend(p, local_sums, partials)
-    cb = _allreduce_cb(allreduce)
+    cb, ctx = _comm_args(allreduce)
     coefs, se, xtxi = np.zeros(p), np.zeros(p), np.zeros((p, p), order="F")
     pre = L.PreLM(L.ptr(coefs), xtxi.ctypes.data_as(L.dp), L.ptr(se), 0, 0, 0, 0, 0, 0)
-    L.check(lib.sglm_fit_lm_external(C.byref(be.struct), cb, None, C.byref(pre)), "sglm_fit_lm_external")
+    L.check(lib.sglm_fit_lm_external(C.byref(be.struct), cb, ctx, C.byref(pre)), "sglm_fit_lm_external")
     return FitLM(coefs, xtxi, se, pre.sse, pre.r2, pre.fstat, pre.sigma, pre.nrow, pre.npart)

@@ -62,14 +62,22 @@ def glm_opts(family="binomial", link="logit", tol=1e-6, verbose=False, max_iter=
 
 
 class Engine:
-    """One HIP device holding one row shard of the design in HBM."""
+    """One HIP device holding one row shard of the design in HBM -- or, with `devices=[...]`,
+    one handle over several devices (sglm_create_multi: row shards per device, one RCCL group
+    all-reduce per iteration; a device listed twice shares the card and sums on the host)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         self._lib = L.load()
         h = C.c_void_p()
-        L.check(self._lib.sglm_create(int(device), C.byref(h)), "sglm_create")
+        if devices is not None:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            L.check(self._lib.sglm_create_multi(devs, len(devices), C.byref(h)), "sglm_create_multi")
+            device = int(devices[0])
+        else:
+            L.check(self._lib.sglm_create(int(device), C.byref(h)), "sglm_create")
         self._h = h
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
         self.n = 0
         self.p = 0
         self._comm_keep = None
@@ -104,12 +112,52 @@ class Engine:
         self.n, self.p = n, p
         return self
 
+    def reserve(self, n: int, p: int, m=False, offset=False, prior=False):
+        """Allocate the resident shard; rows then arrive by set_rows (partition-wise ingest)."""
+        L.check(self._lib.sglm_reserve(self._h, int(n), int(p), int(bool(m)), int(bool(offset)), int(bool(prior))),
+                "sglm_reserve")
+        self.n, self.p = int(n), int(p)
+        return self
+
+    def set_rows(self, row0: int, X, y, m=None, offset=None, prior=None):
+        """Rows [row0, row0 + len(y)) of the reserved shard (one Spark partition's block)."""
+        X = np.asfortranarray(X, dtype=np.float64)
+        nr = X.shape[0]
+        y, m, offset, prior = _vec(y, nr), _vec(m, nr), _vec(offset, nr), _vec(prior, nr)
+        L.check(self._lib.sglm_set_rows(self._h, int(row0), nr, L.ptr(X), max(nr, 1), L.ptr(y), L.ptr(m),
+                                        L.ptr(offset), L.ptr(prior)), "sglm_set_rows")
+        return self
+
     def set_data_device(self, X, y, m=None, offset=None, prior=None):
-        """Torch CUDA tensors (column-major X as X.t().contiguous().t() or an (n, p) F-view)."""
+        """Torch tensors already on this engine's device: X (n, p) column-major (stride(0) == 1,
+        e.g. X.t().contiguous().t()), y / m / offset / prior contiguous length-n vectors, all
+        float64.  The engine copies n doubles from every pointer, so anything else is refused
+        here rather than read past its allocation."""
+        import torch
+        if X.dim() != 2:
+            raise L.IllegalArgumentException("requirement failed: X must be a matrix")
         n, p = X.shape
         ldx = X.stride(1)
-        if X.stride(0) != 1:
-            raise L.IllegalArgumentException("requirement failed: X must be column-major on device")
+        dev = torch.device("cuda", self.device)
+
+        def _ok(t, what):
+            if t.dtype != torch.float64:
+                raise L.IllegalArgumentException(f"requirement failed: {what} must be float64, got {t.dtype}")
+            if not t.is_cuda or t.device != dev:
+                raise L.IllegalArgumentException(f"requirement failed: {what} must live on {dev}, got {t.device}")
+
+        _ok(X, "X")
+        if X.stride(0) != 1 or (p > 1 and ldx < n):
+            raise L.IllegalArgumentException("requirement failed: X must be column-major on device (stride(0) == 1, "
+                                             "leading dimension >= n)")
+        for t, what in ((y, "y"), (m, "m"), (offset, "offset"), (prior, "prior")):
+            if t is None:
+                continue
+            _ok(t, what)
+            if tuple(t.shape) not in ((n,), (n, 1)) or (n > 1 and t.stride(0) != 1):
+                raise L.IllegalArgumentException(f"requirement failed: {what} must be a contiguous vector of "
+                                                 f"length {n}")
+        ldx = max(ldx, n) if p == 1 else ldx
         g = lambda t: None if t is None else C.c_void_p(t.data_ptr())
         L.check(self._lib.sglm_set_data_device(self._h, g(X), n, p, ldx, g(y), g(m), g(offset), g(prior)),
                 "sglm_set_data_device")
@@ -145,6 +193,12 @@ class Engine:
         cb = L.ALLREDUCE_FN(_cb)
         self._comm_keep = cb
         L.check(self._lib.sglm_set_comm(self._h, cb, None, int(bool(on_device))), "sglm_set_comm")
+
+    def set_comm_local(self, rank):
+        """Join an in-process communicator (distributed.LocalComm(n).rank(r)): host threads of
+        one process, one engine each."""
+        self._comm_keep = rank
+        L.check(self._lib.sglm_set_comm(self._h, rank.comm.fn, C.c_void_p(rank.ctx), 0), "sglm_set_comm")
 
     def set_comm_rccl(self, nranks: int, rank: int, unique_id: bytes):
         buf = C.create_string_buffer(bytes(unique_id), 128)
@@ -198,6 +252,32 @@ class Engine:
         L.check(self._lib.sglm_predict(self._h, L.ptr(b), int(bool(add_offset)), L.ptr(out)), "sglm_predict")
         return out
 
+    def predict_glm(self, beta, family="binomial", link="logit", type="response", add_offset=True):
+        """Fitted values of the resident rows on the link or response scale."""
+        o = glm_opts(family, link)
+        b = np.ascontiguousarray(beta, dtype=np.float64).reshape(-1)
+        out = np.empty(self.n)
+        L.check(self._lib.sglm_predict_glm(self._h, L.ptr(b), o.family, o.link, _ptype(type), int(bool(add_offset)),
+                                           L.ptr(out)), "sglm_predict_glm")
+        return out
+
+    def predict_new(self, X, beta, family="gaussian", link="identity", type="link", offset=None, m=None):
+        """Score new rows without touching the resident shard (LM.predict; GLM response scale)."""
+        o = glm_opts(family, link)
+        X = np.asfortranarray(X, dtype=np.float64)
+        if X.ndim != 2:
+            raise L.IllegalArgumentException("requirement failed: X must be a matrix")
+        n, p = X.shape
+        b = np.ascontiguousarray(beta, dtype=np.float64).reshape(-1)
+        if b.shape[0] != p:
+            raise L.IllegalArgumentException(f"requirement failed: Dimension mismatch: X has {p} columns, "
+                                             f"beta {b.shape[0]} rows")
+        offset, m = _vec(offset, n), _vec(m, n)
+        out = np.empty(n)
+        L.check(self._lib.sglm_predict_new(self._h, L.ptr(X), n, p, max(n, 1), L.ptr(b), L.ptr(offset), L.ptr(m),
+                                           o.family, o.link, _ptype(type), L.ptr(out)), "sglm_predict_new")
+        return out
+
     def stats(self) -> dict:
         s = L.Stats()
         L.check(self._lib.sglm_get_stats(self._h, C.byref(s)))
@@ -205,6 +285,12 @@ class Engine:
 
     def reset_stats(self):
         L.check(self._lib.sglm_reset_stats(self._h))
+
+
+def _ptype(t) -> int:
+    if t not in ("link", "response"):
+        raise L.IllegalArgumentException(f"requirement failed: type must be 'link' or 'response', got {t!r}")
+    return L.PREDICT_RESPONSE if t == "response" else L.PREDICT_LINK
 
 
 def device_count() -> int:

@@ -16,7 +16,10 @@ Faithful-to-the-reference behaviour (``strict = True``, the default):
     several (GLM.scala:263 vs 370-371); npart reports the partition count.
 With ``strict = False`` every overload runs on partitioned data and honours its offset.
 The extension families "gaussian", "poisson" and "gamma" (canonical links; prior weights
-through `fit_weighted`) follow R's family objects on the same IRLS skeleton.
+through `fit_weighted`) follow R's family objects on the same IRLS skeleton.  Their `loglik`
+is R's logLik; `aic` stays createObj's -2 loglik + 2p (GLM.scala:70), which counts the
+coefficients only -- R's AIC(glm) for gaussian and Gamma adds 2 for the dispersion parameter,
+so it is 2 higher than `aic` here for those two families.
 """
 from __future__ import annotations
 
@@ -80,6 +83,22 @@ class GLMModel:
     iter: int
     nrow: float
     npart: int
+
+    def predict(self, newData: Frame, type: str = "response", offset: Optional[Frame] = None,
+                m: Optional[Frame] = None, device: int = 0) -> Frame:
+        """Extension (the reference has no GLM predict): (index, value) rows of the
+        linear predictor newX * coefs (+ offset) on the "link" scale, or of mu = unlink(eta, m)
+        on the "response" scale (m = binomial trials, default 1) -- R's predict.glm(type=).
+        Runs on the GPU through sglm_predict_new; newData's columns are taken by the model's
+        names."""
+        _require(len(set(self.xnames) - set(newData.columns)) == 0,
+                 "Not all predictors in the estimation data are in the data to be predicted")
+        fam, lnk = _engine_family_link(self.family, self.link)
+        newX = newData.select(*self.xnames).to_matrix()
+        vals = _engine(device).predict_new(newX, np.asarray(self.coefs, dtype=np.float64).reshape(-1), fam, lnk,
+                                           type, None if offset is None else offset.to_vector(),
+                                           None if m is None else m.to_vector())
+        return Frame({"index": np.arange(len(vals), dtype=np.int64), "value": vals}, newData.npartitions)
 
 
 def _engine_family_link(family: str, link: str):

@@ -46,13 +46,25 @@ class LMModel:
         self.npart = npart
 
     def predict(self, newData: Frame, device: int = 0) -> Frame:
-        """LM.scala:29-61: (index, value) rows of newX * coefs, on the GPU."""
+        """LM.scala:29-61: (index, value) rows of newX * coefs, on the GPU (sglm_predict_new: the
+        new rows stream through a scratch buffer; a design resident on the device stays put).
+
+        As the reference, newX is newData's whole matrix in its own column order (LM.scala:40,
+        54: dfToDenseMatrix / dataFrameToMatrix of newData), so a frame with extra columns fails
+        Breeze's dimension check.  With ``glm.strict = False`` the model's columns are selected
+        by name instead (extension)."""
+        from . import glm as _glm
         _require(len(set(self.xnames) - set(newData.columns)) == 0,
                  "Not all predictors in the estimation data are in the data to be predicted")
-        newX = newData.select(*self.xnames).to_matrix()
-        eng = _engine(device)
-        eng.set_data(newX, np.zeros(newX.shape[0]))
-        vals = eng.predict(np.asarray(self.coefs, dtype=np.float64).reshape(-1))
+        if _glm.strict:
+            newX = newData.to_matrix()
+            if newX.shape[1] != len(self.xnames):
+                raise L.IllegalArgumentException(f"requirement failed: Dimension mismatch: newData has "
+                                                 f"{newX.shape[1]} columns, the model {len(self.xnames)} "
+                                                 f"coefficients (breeze DenseMatrix *)")
+        else:
+            newX = newData.select(*self.xnames).to_matrix()
+        vals = _engine(device).predict_new(newX, np.asarray(self.coefs, dtype=np.float64).reshape(-1))
         return Frame({"index": np.arange(len(vals), dtype=np.int64), "value": vals}, newData.npartitions)
 
     def summary(self) -> "SummaryLM":

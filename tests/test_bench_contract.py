@@ -51,3 +51,35 @@ def test_strong_scaling_point_and_p32_traffic():
     assert callable(bench.strong_1b) and callable(bench.attach_comm)
     t = bench.pmc_traffic(32, 1000, "binomial")
     assert t is not None and 264 * 1000 <= t < 280 * 1000
+
+
+def test_plain_multi_gpu_invocation_launches_its_own_ranks():
+    """`python bench.py --gpus N` without a launcher spawns N rank processes (torch.distributed.run,
+    rendezvous on 127.0.0.1) running this script with the same arguments; under a launcher
+    (WORLD_SIZE set) or at N = 1 it runs in-process."""
+    assert bench.needs_launch({}, 2) and bench.needs_launch({"RANK": "0"}, 8)
+    assert not bench.needs_launch({"WORLD_SIZE": "2"}, 2) and not bench.needs_launch({}, 1)
+    assert bench._gpus_arg(["--steps", "3", "--gpus", "4"]) == 4 and bench._gpus_arg([]) == 1
+    argv = ["--gpus", "4", "--steps", "3", "--warmup", "1"]
+    cmd = bench.launch_cmd(4, argv, 29511)
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29511" in cmd and "--nnodes=1" in cmd
+    assert cmd[-len(argv) - 1].endswith("bench.py") and cmd[-len(argv):] == argv
+
+
+def test_launcher_runs_ranks_with_rank_environment(tmp_path):
+    """The launch path end to end on CPU: torch.distributed.run gives every child the RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* environment bench.py's rank code reads."""
+    import subprocess
+    import sys
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, json\nprint(json.dumps({k: os.environ.get(k) for k in "
+                     "('RANK','LOCAL_RANK','WORLD_SIZE','MASTER_ADDR')}))\n")
+    cmd = bench.launch_cmd(2, [], bench._free_port())
+    cmd[cmd.index(os.path.abspath(bench.__file__))] = str(probe)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    envs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert sorted(e["RANK"] for e in envs) == ["0", "1"]
+    assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)

@@ -166,6 +166,7 @@ def main() -> int:
     ap.add_argument("--cpu-rows", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl")
+    ap.add_argument("--no-load", action="store_true", help="skip the host-to-HBM load probe")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the 1B x 32 strong-scaling point measured after the default workload")
     args = ap.parse_args()
@@ -310,6 +311,14 @@ def main() -> int:
         else:
             out["cpu_baseline"] = None
     eng.close()
+    if not args.no_load:
+        try:  # the H2D load of a host-resident design, reported apart from the fit
+            load = load_probe(dev, p, wl, n)
+        except Exception as exc:
+            log(f"[rank {rank}] load probe failed: {exc}")
+            load = None
+        if rank == 0:
+            out["load"] = load
     if args.workload == "logit256" and not args.no_strong:
         try:  # the north-star 1B-row strong-scaling point, beside the headline (own shard, freed after)
             strong_1b_res = strong_1b(args, dev, world, rank, dist_on, shared, barrier)
@@ -324,6 +333,35 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def load_probe(dev: int, p: int, wl: dict, n_shard: int, sample_bytes: float = 4e9) -> dict:
+    """Time the ingest boundary on a host-resident sample of the workload's shape: pageable host
+    arrays -> sglm_set_data (pinned staging, H2D), as a Spark executor would hand its partitions
+    over.  Reported beside the fit, never inside `value` (the fit runs on HBM-resident data)."""
+    from sparkglm_amd import Engine
+    nvec = 1 + (2 if wl["kind"] == 2 else 0)
+    rows = max(1024, int(sample_bytes / (8 * (p + nvec))))
+    rng = np.random.default_rng(0)
+    X = np.asfortranarray(rng.random((rows, p)))
+    y = rng.random(rows)
+    vec = (rng.random(rows), rng.random(rows)) if wl["kind"] == 2 else (None, None)
+    eng = Engine(dev)
+    try:
+        eng.set_data(X[:1024], y[:1024])  # first-touch (pinned staging allocation) outside the timing
+        eng.reset_stats()
+        t0 = time.perf_counter()
+        eng.set_data(X, y, offset=vec[0], prior=vec[1])
+        wall = time.perf_counter() - t0
+        st = eng.stats()
+    finally:
+        eng.close()
+    gbs = st["load_bytes"] / (st["load_ms"] * 1e-3) / 1e9
+    shard_bytes = 8.0 * n_shard * (p + nvec)
+    return {"sample_rows": rows, "p": p, "bytes": st["load_bytes"], "seconds": st["load_ms"] * 1e-3,
+            "wall_seconds": wall, "gbs": gbs, "path": "pageable host -> 2 x 64 MiB pinned staging -> HBM",
+            "shard_bytes": shard_bytes, "shard_seconds_est": shard_bytes / (gbs * 1e9) if not wl.get("procedural")
+            else None}
 
 
 def _gpus_arg(argv) -> int:

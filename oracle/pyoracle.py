@@ -14,7 +14,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libsglm_oracle.so")
+# SGLM_ORACLE_LIB selects another build of the same library (the sanitizer build, tools/asan_cpu.sh)
+LIB_PATH = os.environ.get("SGLM_ORACLE_LIB") or os.path.join(HERE, "build", "libsglm_oracle.so")
 
 FAMILIES = {"binomial": 0, "gaussian": 1, "poisson": 2, "gamma": 3}
 LINKS = {"logit": 0, "probit": 1, "cloglog": 2, "identity": 3, "log": 4, "inverse": 5}

@@ -104,7 +104,7 @@ def test_gaussian_glm_equals_lm_in_two_iterations(golden):
     c = golden["gaussian"]
     f = po.fit_glm(c["X"], c["y"], "gaussian", "identity")
     r = po.fit_lm(c["X"], c["y"])
-    assert f.iter == 2 and f.dev_trace[2] == f.dev_trace[1]
+    assert f.iter == 2 and abs(f.dev_trace[2] - f.dev_trace[1]) <= 4 * np.spacing(f.dev_trace[1])
     assert rel(f.coefs, r["coefs"]) < 1e-12
     n, p = c["X"].shape
     assert rel(f.stderr * np.sqrt(f.deviance / (n - p)), r["stderr"]) < 1e-10
@@ -124,6 +124,10 @@ def test_oracle_reproduces_golden_vectors(golden):
                        npart=int(npart), nthreads=1)
         s = c["scalars"]
         assert f.iter == int(s[4]), name
+        if os.environ.get("SGLM_ORACLE_LIB"):  # another build (sanitizers, -O1): its own summation order
+            assert rel(f.coefs, c["coefs"]) < 1e-12 and rel(f.stderr, c["stderr"]) < 1e-12, name
+            assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik], s[:4]) < 1e-12, name
+            continue
         np.testing.assert_array_equal(f.coefs, c["coefs"], err_msg=name)
         np.testing.assert_array_equal(f.stderr, c["stderr"], err_msg=name)
         np.testing.assert_array_equal(np.array([f.deviance, f.null_deviance, f.pearson, f.loglik]), s[:4])

@@ -53,6 +53,14 @@ std::string hip_msg(hipError_t e, const char* what) {
     }                                                 \
   } while (0)
 
+// Compensated (Neumaier) accumulation of the scalar partials (host side of rowmath.hpp's
+// neumaier_add): the deviance sum decides the iteration count against an absolute 1e-6.
+inline void neumaier_add(double& s, double& c, double x) {
+  const double t = s + x;
+  c += (std::fabs(s) >= std::fabs(x)) ? (s - t) + x : (x - t) + s;
+  s = t;
+}
+
 double now_ms() {
   using namespace std::chrono;
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
@@ -580,9 +588,9 @@ struct sglm_engine : public Backend {
     std::vector<double> h(nparts);
     HIPCHK(hipMemcpyAsync(h.data(), dpart, sizeof(double) * nparts, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    double s = 0.0;
-    for (int i = 0; i < nparts; ++i) s += h[i];
-    out2[0] = s;
+    double s = 0.0, c = 0.0;
+    for (int i = 0; i < nparts; ++i) neumaier_add(s, c, h[i]);
+    out2[0] = s + c;
     out2[1] = (double)n;
     return allreduce_small(out2, 2);
   }
@@ -813,9 +821,9 @@ struct sglm_engine : public Backend {
     HIPCHK(hipMemcpyAsync(h.data(), dpart, sizeof(double) * h.size(), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (int k = 0; k < NS; ++k) {
-      double v = 0.0;
-      for (int b = 0; b < nb; ++b) v += h[(size_t)b * NS + k];
-      s[k] = v;
+      double v = 0.0, c = 0.0;
+      for (int b = 0; b < nb; ++b) neumaier_add(v, c, h[(size_t)b * NS + k]);
+      s[k] = v + c;
     }
     return allreduce_small(s, NS);
   }

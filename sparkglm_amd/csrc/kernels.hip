@@ -493,14 +493,27 @@ __global__ void reduce_partials_kernel(const double* __restrict__ part, int64_t 
     const double* q = part + src;
     double s = 0.0;
     int g = 0;
-    for (; g + 32 <= nparts; g += 32) {
-      double v[32];
+    if (e < tri + p) {
+      for (; g + 32 <= nparts; g += 32) {
+        double v[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
+        for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) s += v[u];
+        for (int u = 0; u < 32; ++u) s += v[u];
+      }
+      for (; g < nparts; ++g) s += q[(int64_t)g * stride];
+    } else {  // deviance and the other scalars: compensated, in the same order
+      double c = 0.0;
+      for (; g + 32 <= nparts; g += 32) {
+        double v[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) neumaier_add(s, c, v[u]);
+      }
+      for (; g < nparts; ++g) neumaier_add(s, c, q[(int64_t)g * stride]);
+      s += c;
     }
-    for (; g < nparts; ++g) s += q[(int64_t)g * stride];
     out[e] = s;
   }
 }

@@ -146,6 +146,15 @@ __device__ __forceinline__ double binom_logpmf(double mval, double mu, double yv
   return lgamma(n + 1.0) - lgamma(k + 1.0) - lgamma(n - k + 1.0) + k * log(mu) + (n - k) * log1p(-mu);
 }
 
+// Compensated (Neumaier) accumulation for the last, widest levels of the scalar reductions: at
+// 1e9 rows a plain sum of ~256-2048 partials of a ~1e9 deviance carries ~1e-6 of rounding --
+// GLM.scala:281's absolute tol -- so the iteration count would follow the summation order.
+__device__ __forceinline__ void neumaier_add(double& s, double& c, double x) {
+  const double t = s + x;
+  c += (fabs(s) >= fabs(x)) ? (s - t) + x : (x - t) + s;
+  s = t;
+}
+
 struct RowAcc {
   double s[NS];
 };

@@ -421,8 +421,18 @@ __global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stri
       const double* ps = part + src;
       for (int g = g0; g < g1; ++g) s += ps[(int64_t)g * stride];
     } else {
-      const int k = (int)(e - tri - p);
-      for (int g = 0; g < nrow; ++g) s += rowpart[(int64_t)g * NS + k];
+      const int k = (int)(e - tri - p);  // scalars: compensated (rowmath.hpp neumaier_add)
+      double c = 0.0;
+      int g = 0;
+      for (; g + 32 <= nrow; g += 32) {
+        double v[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) v[u] = rowpart[(int64_t)(g + u) * NS + k];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) neumaier_add(s, c, v[u]);
+      }
+      for (; g < nrow; ++g) neumaier_add(s, c, rowpart[(int64_t)g * NS + k]);
+      s += c;
     }
     out[e] = s;
   }

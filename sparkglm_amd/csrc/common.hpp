@@ -55,6 +55,8 @@ struct PassArgs {
   double* partials;     // [grid][stride]
   int64_t stride;
   double* eta_out;      // optional [n]: eta of MODE_IRLS rows (for the final statistics)
+  int stats_in_pass;    // narrow binomial/logit IRLS pass without m: pearson / loglik / bad in the
+                        // pass's scalars instead of the eta store + stats_kernel
   int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math,
                         // 32 no eta store
 };

@@ -140,8 +140,12 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
     }
   }
 
-  rc = be.stats(iter > 0 ? MODE_IRLS : init_mode, beta.data(), ymean, 0.0, o.family, o.link, s.data());
-  if (rc) return rc;
+  if (iter > 0 && be.pass_has_stats()) {  // the last pass computed them at the final mu
+    std::memcpy(s.data(), packed.data() + tri_count(p) + p, sizeof(double) * NS);
+  } else {
+    rc = be.stats(iter > 0 ? MODE_IRLS : init_mode, beta.data(), ymean, 0.0, o.family, o.link, s.data());
+    if (rc) return rc;
+  }
   if (s[S_BAD] > 0) {
     set_error("requirement failed: Binomial(m.toInt, mu).logProbabilityOf(y.toInt) needs 0 <= y <= m, m >= 1");
     return SGLM_EINVAL;

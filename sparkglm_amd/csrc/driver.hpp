@@ -55,6 +55,9 @@ class Backend {
   // Final statistics (pearson, loglik ingredients, ...) at the state of the last pass
   // (MODE_IRLS / init modes) or at beta (MODE_LM_RESID), all-reduced, NS scalars.
   virtual int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) = 0;
+  // True when the last MODE_IRLS pass also delivered the final statistics (pearson, loglik
+  // ingredients, bad) in its packed scalars, so glm_drive needs no stats() pass.
+  virtual bool pass_has_stats() const { return false; }
   // The solver for this backend's systems (default: host).
   virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats

@@ -119,6 +119,8 @@ struct sglm_engine : public Backend {
   int64_t part_cap = 0, red_cap = 0;
   Comm comm;
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
+  bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
+  bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
   // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; SGLM_NARROW=0 disables
@@ -209,6 +211,7 @@ struct sglm_engine : public Backend {
   }
 
   int64_t ncols() const override { return group() ? subs[0]->p : p; }
+  bool pass_has_stats() const override { return group() ? subs[0]->lp_stats : lp_stats; }
   int npart() const override { return group() ? (int)subs.size() : comm.nranks; }
 
   // ---- communicator helpers ----
@@ -663,7 +666,11 @@ struct sglm_engine : public Backend {
     a.ybar = ybar;
     a.partials = dpart;
     a.stride = stride;
-    a.eta_out = (mode == MODE_IRLS && !(dbg & 32)) ? deta : nullptr;
+    // binomial / logit (m = 1) on the narrow path: final statistics in the pass, no eta store
+    a.stats_in_pass = (narrow && mode == MODE_IRLS && family == FAM_BINOMIAL && link == LNK_LOGIT && !dm &&
+                       !force_eta_store) ? 1 : 0;
+    lp_stats = a.stats_in_pass != 0;
+    a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (wide) {
@@ -1070,6 +1077,7 @@ int sglm_create(int device, sglm_engine** out) {
 #endif
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
+  if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
   *out = h;
   return SGLM_OK;
 }

@@ -62,6 +62,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef SGLM_NPRIO
 #define SGLM_NPRIO 4
 #endif
+// Batched Gram phase (all operands, then all VALU, then all MFMAs per block); 0 selects the
+// per-k-step loop for A/B comparisons (tools/ab_narrow.sh).
+#ifndef SGLM_NBATCH
+#define SGLM_NBATCH 0
+#endif
 constexpr int NPRIO = SGLM_NPRIO;
 
 // Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
@@ -94,7 +99,7 @@ struct NGeo {
   static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
   static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB]
   static constexpr int WAVE_LDS = OFF_W + 2 * NRB;   // doubles per wave
-  static constexpr int PSZ = T * 256 + NC + 2;       // one wave partial (tiles | X'Wz | dev, sum w)
+  static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
   static_assert(NW % 4 == 0, "whole waves per SIMD");
   static constexpr int STRIDE = T * 256 + NC + NS;   // global partial (reduce_partials_kernel layout)
@@ -145,7 +150,10 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
 
 // IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
 // IRLS = false instantiation, so the iterations' main loop carries none of their branches.
-template <int P16, int FAM, int LNK, bool IRLS>
+// STATS (binomial / logit IRLS without m, PassArgs::stats_in_pass): the pass also accumulates
+// pearsonCalc / llBinomial at this pass's mu and stores no eta -- the last pass of a fit then
+// carries the final statistics (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass).
+template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
@@ -160,7 +168,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   const int ngrp_stored = ((a.p + 7) / 8 * 8) / G::CPI;  // X stores whole column octets
   constexpr bool irls = IRLS;
   const int mode = IRLS ? (int)MODE_IRLS : a.mode;
-  const bool has_eta = irls && a.eta_out != nullptr;
+  const bool has_eta = irls && !STATS && a.eta_out != nullptr;
 
   // per-lane parts of the DMA source addresses: lane -> (column cc of the group, row pair j);
   // the swizzle repeats every LPER column groups
@@ -194,7 +202,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   double xz[P16];
 #pragma unroll
   for (int b = 0; b < P16; ++b) xz[b] = 0.0;
-  double s_dev = 0.0, s_aux = 0.0;
+  double s_dev = 0.0, s_aux = 0.0, s_pear = 0.0, s_ll = 0.0, s_bad = 0.0;
 
   const int cl = lane & 15, rq = lane >> 4;
   const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
@@ -248,14 +256,63 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+        else if constexpr (STATS)
+          pass_row_logit_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
         else
-          pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2);
+          pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
+                   !IRLS);
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;
     }
 
     NSTAMP(2);
+#if SGLM_NBATCH
+    // ---- Gramian, batched: every operand of the block's NRB/4 k-steps is read into registers,
+    // the LDS buffer is released to the next DMA at once, then the VALU scaling (A = w x) and
+    // X'Wz, then all T * NRB/4 MFMAs back to back.  fp64 VALU and MFMA share the SIMD's DP
+    // pipe (tools/coexec_bench.hip: they serialise), so the per-k-step VALU -> MFMA -> VALU
+    // alternation of the unbatched loop left a dependency bubble at every switch.
+    {
+      constexpr int KS = NRB / 4;
+      double xv[KS][P16], av[KS][P16], wr[KS], wzr[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int r = 4 * s + rq;
+        const double* base = xs + cl * NRB + (r ^ fcl);
+#pragma unroll
+        for (int b = 0; b < P16; ++b) xv[s][b] = base[G::BSTR * b];
+        wr[s] = wl[G::OFF_W + r];
+        wzr[s] = wl[G::OFF_W + NRB + r];
+      }
+      // every LDS read of this buffer has returned: the DMA of block blk + 2 may overwrite it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      NSTAMP(3);
+      if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+      NSTAMP(4);
+      if (do_gram) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int b = 0; b < P16; ++b) {
+            av[s][b] = xv[s][b] * wr[s];
+            xz[b] += xv[s][b] * wzr[s];
+          }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          int t = 0;
+#pragma unroll
+          for (int bi = 0; bi < P16; ++bi)
+#pragma unroll
+            for (int bj = 0; bj <= bi; ++bj, ++t)
+              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s][bi], xv[s][bj], acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+#else
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
     if (do_gram && P16 > 2) {
 #pragma unroll
@@ -329,6 +386,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
     NSTAMP(4);
   }
+#endif
 
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
 #pragma unroll
@@ -337,6 +395,11 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   for (int o = 1; o < 64; o <<= 1) {
     s_dev += __shfl_xor(s_dev, o);
     s_aux += __shfl_xor(s_aux, o);
+    if constexpr (STATS) {
+      s_pear += __shfl_xor(s_pear, o);
+      s_ll += __shfl_xor(s_ll, o);
+      s_bad += __shfl_xor(s_bad, o);
+    }
   }
 
   // ---- fixed-order fold over the NW waves in LDS: while n > 1, waves [h, n) (h = ceil(n/2))
@@ -359,6 +422,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       if (lane == 0) {
         reg[G::T * 256 + G::NC] = s_dev;
         reg[G::T * 256 + G::NC + 1] = s_aux;
+        reg[G::T * 256 + G::NC + 2] = s_pear;
+        reg[G::T * 256 + G::NC + 3] = s_ll;
+        reg[G::T * 256 + G::NC + 4] = s_bad;
       }
     }
     __syncthreads();
@@ -372,6 +438,11 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       for (int b = 0; b < P16; ++b) xz[b] += reg[G::T * 256 + 16 * b + (lane & 15)];
       s_dev += reg[G::T * 256 + G::NC];
       s_aux += reg[G::T * 256 + G::NC + 1];
+      if constexpr (STATS) {
+        s_pear += reg[G::T * 256 + G::NC + 2];
+        s_ll += reg[G::T * 256 + G::NC + 3];
+        s_bad += reg[G::T * 256 + G::NC + 4];
+      }
     }
     __syncthreads();
     n = h;
@@ -386,13 +457,22 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
       for (int b = 0; b < P16; ++b) out[G::T * 256 + 16 * b + lane] = xz[b];
     }
-    if (lane < NS) out[G::T * 256 + G::NC + lane] = lane == S_DEV ? s_dev : (lane == S_SUMW ? s_aux : 0.0);
+    if (lane < NS)
+      out[G::T * 256 + G::NC + lane] = lane == S_DEV       ? s_dev
+                                       : lane == S_SUMW    ? s_aux
+                                       : lane == S_PEARSON ? s_pear
+                                       : lane == S_LL      ? s_ll
+                                       : lane == S_BAD     ? s_bad
+                                                           : 0.0;
   }
 }
 
 template <int P16, int FAM, int LNK>
 void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st) {
-  if (a.mode == MODE_IRLS)
+  if (a.mode == MODE_IRLS && FAM == FAM_BINOMIAL && LNK == LNK_LOGIT && a.stats_in_pass && !a.m)
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, FAM == FAM_BINOMIAL && LNK == LNK_LOGIT>), gr, bl, 0, st,
+                       a);
+  else if (a.mode == MODE_IRLS)
     hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true>), gr, bl, 0, st, a);
   else
     hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false>), gr, bl, 0, st, a);

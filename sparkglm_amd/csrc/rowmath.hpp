@@ -14,6 +14,10 @@
 
 #include "common.hpp"
 
+#ifndef SGLM_ESTRIN
+#define SGLM_ESTRIN 0  // 0: Horner forms of exp_small / log_pos (A/B builds)
+#endif
+
 namespace sglm {
 
 // Breeze Gaussian(0,1) as used by the probit link.
@@ -59,6 +63,16 @@ __device__ __forceinline__ double log_pos(double x) {
   const double f = m - 1.0;
   const double s = f * rcp_pos(m + 1.0);
   const double z = s * s;
+#if SGLM_ESTRIN
+  // the same polynomial in Estrin's scheme: dependency depth 4 instead of 9 (the row stage is
+  // latency-bound beside the partner wave's MFMAs on the shared fp64 pipe)
+  const double z2 = z * z;
+  const double a0 = fma(sc(1.0 / 5.0), z, sc(1.0 / 3.0)), a1 = fma(sc(1.0 / 9.0), z, sc(1.0 / 7.0));
+  const double a2 = fma(sc(1.0 / 13.0), z, sc(1.0 / 11.0)), a3 = fma(sc(1.0 / 17.0), z, sc(1.0 / 15.0));
+  const double z4 = z2 * z2;
+  const double b0 = fma(a1, z2, a0), b1 = fma(a3, z2, a2);
+  const double q = fma(fma(sc(1.0 / 19.0), z4, b1), z4, b0);
+#else
   double q = sc(1.0 / 19.0);
   q = fma(q, z, sc(1.0 / 17.0));
   q = fma(q, z, sc(1.0 / 15.0));
@@ -68,6 +82,7 @@ __device__ __forceinline__ double log_pos(double x) {
   q = fma(q, z, sc(1.0 / 7.0));
   q = fma(q, z, sc(1.0 / 5.0));
   q = fma(q, z, sc(1.0 / 3.0));
+#endif
   const double lm = fma(2.0 * s, z * q, 2.0 * s);
   const double kd = (double)k;
   return fma(kd, sc(6.93147180559945286227e-01), fma(kd, sc(2.31904681384629955842e-17), lm));
@@ -80,6 +95,20 @@ __device__ __forceinline__ double exp_small(double x) {
   const double kf = rint(x * sc(1.44269504088896338700));
   double r = fma(-kf, sc(6.93147180559945286227e-01), x);
   r = fma(-kf, sc(2.31904681384629955842e-17), r);
+#if SGLM_ESTRIN
+  // Estrin's scheme (depth 5 instead of 13; see log_pos)
+  const double r2 = r * r;
+  const double a0 = r + 1.0, a1 = fma(sc(1.0 / 6.0), r, 0.5);
+  const double a2 = fma(sc(1.0 / 120.0), r, sc(1.0 / 24.0)), a3 = fma(sc(1.0 / 5040.0), r, sc(1.0 / 720.0));
+  const double a4 = fma(sc(1.0 / 362880.0), r, sc(1.0 / 40320.0));
+  const double a5 = fma(sc(1.0 / 39916800.0), r, sc(1.0 / 3628800.0));
+  const double a6 = fma(sc(1.0 / 6227020800.0), r, sc(1.0 / 479001600.0));
+  const double r4 = r2 * r2;
+  const double b0 = fma(a1, r2, a0), b1 = fma(a3, r2, a2), b2 = fma(a5, r2, a4);
+  const double r8 = r4 * r4;
+  const double d0 = fma(b1, r4, b0), d1 = fma(a6, r4, b2);
+  const double q = fma(d1, r8, d0);
+#else
   double q = sc(1.0 / 6227020800.0);  // 1/13!
   q = fma(q, r, sc(1.0 / 479001600.0));
   q = fma(q, r, sc(1.0 / 39916800.0));
@@ -94,6 +123,7 @@ __device__ __forceinline__ double exp_small(double x) {
   q = fma(q, r, 0.5);
   q = fma(q, r, 1.0);
   q = fma(q, r, 1.0);
+#endif
   return __builtin_amdgcn_ldexp(q, (int)kf);
 }
 
@@ -205,12 +235,14 @@ __device__ __noinline__ RowWZ pass_row_ref(int fam, int lnk, int mode, double et
 // The row stage of the fused pass (zwCreateBinomial, GLM.scala:359-395 / the single-
 // partition loop body GLM.scala:282-301): w and w*z for the Gramian, and the deviance.
 // LM gram mode: w = 1, z = y, and the sums of y and of rows (LM.scala:142-155, 167).
-// small_exp (a compile-time constant at every call site) selects exp_small over libm's exp:
+// small_exp and init_fast are compile-time constants at every call site.
+// small_exp selects exp_small over libm's exp:
 // measured faster in the p <= 32 narrow pass (-1 %), slower at p = 64 (+4 %) and neutral in
 // the fused / wide kernels, so only the p <= 32 narrow variants set it.
 __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta, double y, double m, double off,
                                          double pw, double mu0, double ybar, bool has_m, double& w, double& wz,
-                                         double& s_dev, double& s_aux, bool small_exp = false) {
+                                         double& s_dev, double& s_aux, bool small_exp = false,
+                                         bool init_fast = false) {
   (void)ybar;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT && mode == MODE_IRLS && !has_m && fabs(eta) < 8.0 && y >= 0.0 &&
       y <= 1.0) {
@@ -267,12 +299,42 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
     s_aux += 1.0;
     return;
   }
+  if (init_fast && fam == FAM_BINOMIAL && mode != MODE_IRLS && mode != MODE_LM_GRAM && !has_m && y >= 0.0 &&
+      y <= 1.0) {
+    // The initial pass (GLM.scala:263-272, 429-444): mu = mu0 (fitSingle) or unlink(link(mu0))
+    // (fitMultiple) is the same for every row, so link, lPrime and the variance are loop
+    // invariants (hoisted out of the pass's row loop); per row only z and the deviance remain.
+    // (init_fast: set by the narrow kernel's non-IRLS instantiation only, whose loop the
+    // invariants are hoisted out of; the fused / wide kernels keep pass_row_ref for it.)
+    // max(y, 1) = max(1 - y, 1) = 1 for 0 <= y <= 1, so devBinomial's logs are invariant too --
+    // the expressions below are the reference's own, operation for operation (pass_row_ref).
+    const double e0 = link_fn(fam, lnk, mu0, 1.0);
+    const double mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, e0, 1.0);
+    const double g = lprime_fn(fam, lnk, mu, 1.0);
+    const double w0 = 1.0 / (variance_fn(fam, mu, 1.0) * (g * g));
+    const double l1 = log(1.0 / mu0), l0 = log(1.0 / (1.0 + (-1.0 * mu0)));
+    w = pw * w0;
+    const double z = (e0 + ((y + (-1.0 * mu)) * g)) + (-1.0 * off);
+    wz = w * z;
+    const double my = 1.0 + (-1.0 * y);
+    s_dev += pw * ((y * l1) + (my * l0));
+    s_aux += pw;
+    return;
+  }
   const RowWZ r = pass_row_ref(fam, lnk, mode, eta, y, m, off, pw, mu0);
   w = r.w;
   wz = r.wz;
   s_dev += r.dev;
   s_aux += pw;
 }
+
+// Logit with m = 1, in-pass final statistics (PassArgs::stats_in_pass): the IRLS row stage of
+// pass_row plus stats_row's pearsonCalc / llBinomial terms at the same mu, sharing one exp, one
+// reciprocal and one log -- the pass then needs no eta store and no stats_kernel pass.  Rows
+// outside the fast range take both reference-order functions.
+__device__ __forceinline__ void pass_row_logit_stats(double eta, double y, double off, double pw, double& w, double& wz,
+                                                     double& s_dev, double& s_aux, double& s_pear, double& s_ll,
+                                                     double& s_bad, bool small_exp);
 
 // The reference operation order of the final statistics (pearsonCalc GLM.scala:90-101,
 // llBinomial :132-143, devBinomial :162-170, the R families' loglik ingredients), out of line
@@ -349,6 +411,35 @@ __device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta
   const RowAcc r = stats_row_ref(fam, lnk, mode, eta, y, m, pw, mu0, has_m);
 #pragma unroll
   for (int k = 0; k < NS; ++k) acc.s[k] += r.s[k];
+}
+
+__device__ __forceinline__ void pass_row_logit_stats(double eta, double y, double off, double pw, double& w, double& wz,
+                                                     double& s_dev, double& s_aux, double& s_pear, double& s_ll,
+                                                     double& s_bad, bool small_exp) {
+  if (fabs(eta) < 8.0 && y >= 0.0 && y <= 1.0) {
+    const double e = small_exp ? exp_small(-eta) : exp(-eta);
+    const double u = 1.0 + e;
+    const double t = rcp_pos(u);
+    const double v = e * t * t;
+    const double L = fma(e - (u - 1.0), t, log_pos(u));  // log1p(e) = -log(mu)
+    w = pw * v;
+    wz = pw * (v * (eta - off) + (y - t));
+    s_dev += pw * (L + (1.0 - y) * eta);
+    s_aux += pw;
+    const double r = y - t;
+    s_pear += pw * (r * r) * rcp_pos(v);
+    s_ll += pw * ((int)y == 1 ? -L : -L - eta);
+    return;
+  }
+  const RowWZ r = pass_row_ref(FAM_BINOMIAL, LNK_LOGIT, MODE_IRLS, eta, y, 1.0, off, pw, 0.0);
+  w = r.w;
+  wz = r.wz;
+  s_dev += r.dev;
+  s_aux += pw;
+  const RowAcc a = stats_row_ref(FAM_BINOMIAL, LNK_LOGIT, MODE_IRLS, eta, y, 1.0, pw, 0.0, false);
+  s_pear += a.s[S_PEARSON];
+  s_ll += a.s[S_LL];
+  s_bad += a.s[S_BAD];
 }
 
 }  // namespace sglm

@@ -8,6 +8,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -62,6 +63,18 @@ __global__ void __launch_bounds__(64 * NW, 1) stream_kernel(const double* X, int
   }
 }
 
+// Fill with random-looking doubles in (-1, 1): HBM / fabric power (and with it the sustained
+// rate) depends on the data; an all-zero image measures an optimistic number.
+__global__ void fill_kernel(double* x, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    x[i] = (double)(z >> 11) * 0x1.0p-52 - 1.0;
+  }
+}
+
 static double* X;
 static double* out;
 static unsigned long long* clk;
@@ -93,11 +106,15 @@ void run(int grid) {
 int main() {
   const size_t bytes = sizeof(double) * NROWS * 32;
   if (hipMalloc(&X, bytes) != hipSuccess) return 1;
-  hipMemset(X, 0, bytes);
+  if (getenv("STREAM_ZERO")) hipMemset(X, 0, bytes);
+  else hipLaunchKernelGGL(fill_kernel, dim3(65536), dim3(256), 0, 0, X, (int64_t)NROWS * 32);
+  hipDeviceSynchronize();
   hipMalloc(&out, sizeof(double) * 512 * 1024);
   hipMalloc(&clk, sizeof(unsigned long long) * 2 * 512);
   // p = 32
   run<32, 32, 2, 8, false>(256);  // current narrow geometry at p <= 32
+  run<64, 32, 2, 4, false>(256);  // 512-byte column segments
+  run<128, 32, 2, 2, false>(256); // 1 KiB column segments
   run<32, 32, 2, 8, true>(256);
   run<16, 32, 2, 8, false>(256);
   run<16, 32, 4, 8, false>(256);

@@ -62,6 +62,15 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef SGLM_NPRIO
 #define SGLM_NPRIO 4
 #endif
+// Diagonal 16x16 tiles on v_mfma_f64_4x4x4f64 (4 blocks): three MFMAs of 16 cycles cover the
+// 10 lower 4x4 sub-blocks of a symmetric tile (B operand rotated by 0, 4, 8 lanes within each
+// 16-lane row, read from LDS at the rotated column) instead of one 64-cycle 16x16x4 that also
+// computes the upper half.  Measured (tools/ab_narrow2.sh, round 2): correct, but p = 32
+// +1 % and p = 64 +39 % per pass -- the 4x4x4 accumulation chains and the extra rotated-operand
+// LDS reads cost more than the 25 % of diagonal-tile MFMA cycles they save.  Off by default.
+#ifndef SGLM_NDIAG44
+#define SGLM_NDIAG44 0
+#endif
 // Batched Gram phase (all operands, then all VALU, then all MFMAs per block); 0 selects the
 // per-k-step loop for A/B comparisons (tools/ab_narrow.sh).
 #ifndef SGLM_NBATCH
@@ -148,6 +157,29 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
     __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
 }
 
+// One k-step (4 rows) of the lower-triangular Gram: off-diagonal tiles on 16x16x4; diagonal
+// tiles on 16x16x4 or (SGLM_NDIAG44) on three 4x4x4 MFMAs into acc[t][0..2]: with A = w x of
+// the tile's columns (lane 16k + 4 blk + m: row k, column 4 blk + m -- the 16x16x4 A layout),
+// the B operand rotated by rr groups of 4 lanes (column 4 ((blk + rr) & 3) + n) gives block blk
+// the 4x4 sub-block (blk, (blk + rr) & 3) of the tile in lane 16 m + 4 blk + n.
+template <int P16>
+__device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double (&av)[P16], const double (&xv)[P16],
+                                           const double (&x1)[P16], const double (&x2)[P16]) {
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < P16; ++bi)
+#pragma unroll
+    for (int bj = 0; bj <= bi; ++bj, ++t) {
+      if (SGLM_NDIAG44 && bi == bj) {
+        acc[t][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], xv[bi], acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x1[bi], acc[t][1], 0, 0, 0);
+        acc[t][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x2[bi], acc[t][2], 0, 0, 0);
+      } else {
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+      }
+    }
+}
+
 // IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
 // IRLS = false instantiation, so the iterations' main loop carries none of their branches.
 // STATS (binomial / logit IRLS without m, PassArgs::stats_in_pass): the pass also accumulates
@@ -206,6 +238,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 
   const int cl = lane & 15, rq = lane >> 4;
   const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
+  // diagonal-tile B operands rotated by 4 and 8 columns within the 16-column block
+  const int cl1 = (cl + 4) & 15, cl2 = (cl + 8) & 15;
+  const int off1 = cl1 * NRB - cl * NRB, off2 = cl2 * NRB - cl * NRB;
+  const int fc1 = swz<NRB>(cl1), fc2 = swz<NRB>(cl2);
   const bool do_rows = !(SGLM_DBG(a) & 1), do_gram = !(SGLM_DBG(a) & 2), do_dma = !(SGLM_DBG(a) & 4);
 
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
@@ -320,43 +356,60 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const int r = 4 * s + rq;
         const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + NRB + r];
         const double* base = xs + cl * NRB + (r ^ fcl);
-        double xv[P16], av[P16];
+        const double* base1 = xs + cl * NRB + off1 + (r ^ fc1);
+        const double* base2 = xs + cl * NRB + off2 + (r ^ fc2);
+        double xv[P16], av[P16], x1[P16], x2[P16];
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
           xv[b] = base[G::BSTR * b];
+          if (SGLM_NDIAG44) {
+            x1[b] = base1[G::BSTR * b];
+            x2[b] = base2[G::BSTR * b];
+          }
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
-        int t = 0;
-#pragma unroll
-        for (int bi = 0; bi < P16; ++bi)
-#pragma unroll
-          for (int bj = 0; bj <= bi; ++bj, ++t)
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+        gram_kstep<P16>(acc, av, xv, x1, x2);
       }
     }
     if (do_gram && P16 <= 2) {
       // p <= 32 (3 MFMAs per k-step): software-pipelined -- k-step s+1's operands are read from
       // LDS before k-step s's MFMAs issue, so their latency hides under the MFMA pipe.  (At
       // p > 32, 10 MFMAs per k-step already cover it; measured +1.4 % there, mean of 5, not kept.)
-      double xv[P16], wr, wzr;
+      double xv[P16], x1[P16], x2[P16], wr, wzr;
       {
         const double* base = xs + cl * NRB + (rq ^ fcl);
+        const double* base1 = xs + cl * NRB + off1 + (rq ^ fc1);
+        const double* base2 = xs + cl * NRB + off2 + (rq ^ fc2);
         wr = wl[G::OFF_W + rq];
         wzr = wl[G::OFF_W + NRB + rq];
 #pragma unroll
-        for (int b = 0; b < P16; ++b) xv[b] = base[G::BSTR * b];
+        for (int b = 0; b < P16; ++b) {
+          xv[b] = base[G::BSTR * b];
+          if (SGLM_NDIAG44) {
+            x1[b] = base1[G::BSTR * b];
+            x2[b] = base2[G::BSTR * b];
+          }
+        }
       }
 #pragma unroll
       for (int s = 0; s < NRB / 4; ++s) {
-        double xn[P16], wrn = 0.0, wzrn = 0.0;
+        double xn[P16], xn1[P16], xn2[P16], wrn = 0.0, wzrn = 0.0;
         if (s + 1 < NRB / 4) {
           const int r = 4 * (s + 1) + rq;
           const double* base = xs + cl * NRB + (r ^ fcl);
+          const double* base1 = xs + cl * NRB + off1 + (r ^ fc1);
+          const double* base2 = xs + cl * NRB + off2 + (r ^ fc2);
           wrn = wl[G::OFF_W + r];
           wzrn = wl[G::OFF_W + NRB + r];
 #pragma unroll
-          for (int b = 0; b < P16; ++b) xn[b] = base[G::BSTR * b];
+          for (int b = 0; b < P16; ++b) {
+            xn[b] = base[G::BSTR * b];
+            if (SGLM_NDIAG44) {
+              xn1[b] = base1[G::BSTR * b];
+              xn2[b] = base2[G::BSTR * b];
+            }
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
         double av[P16];
@@ -365,16 +418,17 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
-        int t = 0;
-#pragma unroll
-        for (int bi = 0; bi < P16; ++bi)
-#pragma unroll
-          for (int bj = 0; bj <= bi; ++bj, ++t)
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+        gram_kstep<P16>(acc, av, xv, x1, x2);
         __builtin_amdgcn_sched_barrier(0);
         if (s + 1 < NRB / 4) {
 #pragma unroll
-          for (int b = 0; b < P16; ++b) xv[b] = xn[b];
+          for (int b = 0; b < P16; ++b) {
+            xv[b] = xn[b];
+            if (SGLM_NDIAG44) {
+              x1[b] = xn1[b];
+              x2[b] = xn2[b];
+            }
+          }
           wr = wrn;
           wzr = wzrn;
         }
@@ -449,10 +503,28 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   }
   if (wv == 0) {
     double* out = a.partials + (int64_t)blockIdx.x * a.stride;
+    int t = 0;
 #pragma unroll
-    for (int t = 0; t < G::T; ++t)
+    for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t][j];
+      for (int bj = 0; bj <= bi; ++bj, ++t) {
+        if (SGLM_NDIAG44 && bi == bj) {
+          // 4x4x4 layout -> tile element (i, j) at 16 i + j (reduce_partials_kernel reads i >= j):
+          // rotation rr, lane 16 m + 4 blk + n holds sub-block (blk, J = (blk + rr) & 3), element
+          // (4 blk + m, 4 J + n); an upper sub-block (blk < J) is stored transposed (the tile is
+          // symmetric), rotation 2's two upper sub-blocks duplicate lower ones and are dropped
+          const int m = lane >> 4, blk = (lane >> 2) & 3, n = lane & 3;
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            const int J = (blk + rr) & 3, i = 4 * blk + m, j = 4 * J + n;
+            if (rr == 0 || blk > J) out[t * 256 + 16 * i + j] = acc[t][rr];
+            else if (rr == 1) out[t * 256 + 16 * j + i] = acc[t][rr];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t][j];
+        }
+      }
     if (lane < 16) {
 #pragma unroll
       for (int b = 0; b < P16; ++b) out[G::T * 256 + 16 * b + lane] = xz[b];

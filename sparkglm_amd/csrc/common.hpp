@@ -91,6 +91,9 @@ struct WideRowArgs {
   double* eta_out;      // optional [n]
   double* row_partials; // [grid][NS]
   ProcX proc;
+  int64_t r_begin, r_end;  // rows [r_begin, r_end) of this launch (multiples of 4; r_end may pass n_pad)
+  double* xs_out;       // procedural chunks: the generated X rows stored here (column-major,
+  int64_t xs_ld;        //   leading dimension xs_ld, local row = row - r_begin), else null
 };
 
 // One run of consecutive 16-row blocks of one super-tile, processed by one workgroup of

@@ -127,6 +127,14 @@ struct sglm_engine : public Backend {
   bool narrow = false, allow_narrow = true;
   // procedural shard (sglm_synth_procedural): X regenerated in the wide kernels, not stored
   ProcX procx{};
+  // procedural shards in chunks (setup_proc_chunks): each pass generates C rows of X at a time
+  // into an HBM scratch (the row kernel, while it forms eta) and runs the resident Gram kernels
+  // over it -- X is generated once per pass instead of once per super-tile that reads it
+  int64_t ch_rows = 0;  // rows per chunk (multiple of 32); 0: in-kernel generation (PROC kernels)
+  int nch = 0;
+  std::vector<hipEvent_t> evch;  // [2 * nch]: row-kernel span of each chunk
+  double *dxsc = nullptr, *dchunks = nullptr;
+  bool allow_chunks = true;  // SGLM_PROC_CHUNKS=0 disables
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
   int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
@@ -175,6 +183,12 @@ struct sglm_engine : public Backend {
     n = p = n_pad = nblocks = 0;
     rows_loaded = 0;
     procx = ProcX{};
+    for (double** ptr : {&dxsc, &dchunks}) {
+      if (*ptr) (void)hipFree(*ptr);
+      *ptr = nullptr;
+    }
+    ch_rows = 0;
+    nch = 0;
   }
   void release() {
     (void)hipSetDevice(device);
@@ -202,6 +216,8 @@ struct sglm_engine : public Backend {
     }
     if (comm.nccl) (void)ncclCommDestroy(comm.nccl);
     comm.nccl = nullptr;
+    for (hipEvent_t e : evch) (void)hipEventDestroy(e);
+    evch.clear();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
@@ -278,7 +294,7 @@ struct sglm_engine : public Backend {
   // into ggrid equal segments; a segment's runs inside one super-tile are its pieces.
   // Pieces are numbered in line order, so the partial slots of a super-tile are consecutive.
   int build_wide_schedule() {
-    const int64_t nb = n_pad / WIDE_RB;
+    const int64_t nb = (nch > 0 ? ch_rows : n_pad) / WIDE_RB;
     std::vector<int> str((size_t)nst * 2, 0);
     free_schedule();
     int slot = 0;
@@ -348,6 +364,42 @@ struct sglm_engine : public Backend {
     }
     if (!evm) HIPCHK(hipEventCreate(&evm));
     return SGLM_OK;
+  }
+
+  // Chunked procedural passes: the largest chunk the free HBM holds (minus a margin), balanced
+  // over the chunks; w / w*z cover nch * ch_rows rows (zero past n_pad).  Called once procx is set.
+  int setup_proc_chunks() {
+    if (!procx.on || !allow_chunks) return SGLM_OK;
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    const int64_t ncols8 = (p + 7) / 8 * 8;
+    const size_t margin = (size_t)4 << 30;
+    const int64_t cap_rows = fr > margin ? (int64_t)((fr - margin) / (sizeof(double) * (size_t)ncols8)) : 0;
+    int64_t c = std::min<int64_t>(n_pad, cap_rows / 32 * 32);
+    if (c < std::min<int64_t>(n_pad, (int64_t)1 << 20)) return SGLM_OK;  // too little room: in-kernel generation
+    const int64_t k = (n_pad + c - 1) / c;
+    c = ((n_pad + k - 1) / k + 31) / 32 * 32;
+    ch_rows = c;
+    nch = (int)((n_pad + c - 1) / c);
+    HIPCHK(hipMalloc(&dxsc, sizeof(double) * (size_t)c * (size_t)ncols8));
+    HIPCHK(hipMemsetAsync(dxsc, 0, sizeof(double) * (size_t)c * (size_t)ncols8, st));
+    const int64_t span = (int64_t)nch * c;  // w / w*z rows the chunks address
+    if (span > n_pad) {
+      for (double** q : {&dw, &dwz}) {
+        if (*q) HIPCHK(hipFree(*q));
+        *q = nullptr;
+        HIPCHK(hipMalloc(q, sizeof(double) * (size_t)span));
+        HIPCHK(hipMemsetAsync(*q, 0, sizeof(double) * (size_t)span, st));
+      }
+    }
+    HIPCHK(hipMalloc(&dchunks, sizeof(double) * (size_t)nch * (size_t)packed_len(p)));
+    while (evch.size() < (size_t)2 * nch) {
+      hipEvent_t e = nullptr;
+      HIPCHK(hipEventCreate(&e));
+      evch.push_back(e);
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return ensure_wide_workspace();  // the Gram schedule for ch_rows-row chunks
   }
 
   int ensure_workspace() {
@@ -627,7 +679,15 @@ struct sglm_engine : public Backend {
     HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
     if (wide) {
       float km = 0.f;
-      HIPCHK(hipEventElapsedTime(&km, ev0, evm));
+      if (nch > 0) {  // chunked procedural pass: the row kernels' spans, the rest is Gram
+        for (int c = 0; c < nch; ++c) {
+          float kc = 0.f;
+          HIPCHK(hipEventElapsedTime(&kc, evch[(size_t)2 * c], evch[(size_t)2 * c + 1]));
+          km += kc;
+        }
+      } else {
+        HIPCHK(hipEventElapsedTime(&km, ev0, evm));
+      }
       row_ms += km;
       gram_ms += k1 - km;
     }
@@ -695,8 +755,8 @@ struct sglm_engine : public Backend {
       r.eta_out = (mode == MODE_IRLS) ? deta : nullptr;
       r.row_partials = drp;
       r.proc = procx;
-      HIPCHK(launch_wide_rows(r, rgrid, st));
-      HIPCHK(hipEventRecord(evm, st));
+      r.r_begin = 0;
+      r.r_end = n_pad;
       WideGramArgs g{};
       g.X = dX;
       g.ld = n_pad;
@@ -707,6 +767,37 @@ struct sglm_engine : public Backend {
       g.stride = wstride;
       g.dbg = dbg;
       g.proc = procx;
+      if (nch > 0) {  // procedural shard in chunks: generate C rows into the scratch, resident Gram over it
+        const int64_t plen = packed_len(p);
+        g.X = dxsc;
+        g.ld = ch_rows;
+        g.proc = ProcX{};
+        r.xs_out = dxsc;
+        r.xs_ld = ch_rows;
+        for (int c = 0; c < nch; ++c) {
+          r.r_begin = (int64_t)c * ch_rows;
+          r.r_end = r.r_begin + ch_rows;
+          HIPCHK(hipEventRecord(evch[(size_t)2 * c], st));
+          HIPCHK(launch_wide_rows(r, rgrid, st));
+          HIPCHK(hipEventRecord(evch[(size_t)2 * c + 1], st));
+          g.w = dw + r.r_begin;
+          g.wz = dwz + r.r_begin;
+          for (int kind = 0; kind < 2; ++kind) {
+            if (!has_sched[kind]) continue;
+            g.pieces = dpieces[kind];
+            g.wg_begin = dwgb[kind];
+            HIPCHK(launch_wide_gram(g, kind == 1, ggrid, st));
+          }
+          HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dchunks + (int64_t)c * plen, st));
+        }
+        HIPCHK(hipEventRecord(evm, st));  // unused in chunked timing (pass_timing sums evch)
+        HIPCHK(hipEventRecord(ev1, st));
+        HIPCHK(launch_sum_chunks(dchunks, nch, (int)p, dred, st));
+        HIPCHK(hipEventRecord(ev2, st));
+        return SGLM_OK;
+      }
+      HIPCHK(launch_wide_rows(r, rgrid, st));
+      HIPCHK(hipEventRecord(evm, st));
       for (int kind = 0; kind < 2; ++kind) {
         if (!has_sched[kind]) continue;
         g.pieces = dpieces[kind];
@@ -1078,6 +1169,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
+  if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   *out = h;
   return SGLM_OK;
 }
@@ -1248,6 +1340,7 @@ static int synth_impl(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t
     h->procx.n = n;
     h->procx.kx = splitmix64_host(seed);
     h->procx.scale = scale;
+    if (int rc2 = h->setup_proc_chunks()) return rc2;
   }
   return SGLM_OK;
 }

@@ -38,6 +38,7 @@ int wide_gram_wg_per_cu();
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st);
 hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,
                               int nrow, double* out, hipStream_t st);
+hipError_t launch_sum_chunks(const double* chunks, int nch, int p, double* out, hipStream_t st);
 hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st);
 
 }  // namespace sglm

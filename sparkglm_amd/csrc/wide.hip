@@ -310,14 +310,46 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
 #endif
   constexpr int RPT = SGLM_WIDE_RPT;  // rows per thread (even, divides 32)
   __shared__ double red[4][2];
-  const int64_t nq = a.n_pad / RPT;  // row quads (n_pad is a multiple of 32)
+  const int64_t q0 = a.r_begin / RPT, nq = (a.r_end - a.r_begin) / RPT;  // row quads of this launch
   const int64_t per = (nq + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = per * blockIdx.x, hi = (lo + per < nq) ? lo + per : nq;
+  const int64_t lo = q0 + per * blockIdx.x, hi = (per * blockIdx.x + per < nq) ? lo + per : q0 + nq;
   double s_dev = 0.0, s_aux = 0.0;
   for (int64_t iq = lo + threadIdx.x; iq < hi; iq += blockDim.x) {
     const int64_t i = RPT * iq;
     double eta[RPT] = {};
-    if (a.mode == MODE_IRLS) {
+    if (a.xs_out) {  // procedural chunk: generate the rows once, store them for the Gram kernels
+      double* xo = a.xs_out + (i - a.r_begin);
+      double e[RPT][4] = {};
+      for (int j = 0; j < a.p; ++j) {
+        const double b = (a.mode == MODE_IRLS) ? a.beta[j] : 0.0;
+        double x[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+          x[r] = (i + r < a.n) ? proc_x(a.proc, i + r, j) : 0.0;
+          e[r][j & 3] += x[r] * b;  // the resident path's partial-sum order (j + q, q = j & 3)
+        }
+#pragma unroll
+        for (int h = 0; h < RPT / 2; ++h) *(double2*)(xo + (int64_t)j * a.xs_ld + 2 * h) = double2{x[2 * h], x[2 * h + 1]};
+      }
+      if (a.mode == MODE_IRLS) {
+        const int pt = a.p & ~3;  // columns past the last whole quad went to e[r][0] in the resident order
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+          double t[4] = {0.0, 0.0, 0.0, 0.0};
+          // recompute in the resident order only when p is not a multiple of 4 (exactness)
+          if (pt != a.p) {
+            int j = 0;
+            for (; j + 4 <= a.p; j += 4)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) t[q] += xo[(int64_t)(j + q) * a.xs_ld + r] * a.beta[j + q];
+            for (; j < a.p; ++j) t[0] += xo[(int64_t)j * a.xs_ld + r] * a.beta[j];
+            eta[r] = (t[0] + t[1]) + (t[2] + t[3]);
+          } else {
+            eta[r] = (e[r][0] + e[r][1]) + (e[r][2] + e[r][3]);
+          }
+        }
+      }
+    } else if (a.mode == MODE_IRLS) {
       double e[RPT][4] = {};
       if (a.proc.on) {  // procedural design: same partial-sum order as the resident image
 #pragma unroll
@@ -438,6 +470,21 @@ __global__ void wide_reduce_kernel(const double* __restrict__ part, int64_t stri
   }
 }
 
+// Sum of the per-chunk packed results of a chunked procedural pass, in chunk order (scalars
+// compensated, as wide_reduce_kernel's).
+__global__ void sum_chunks_kernel(const double* __restrict__ chunks, int nch, int64_t len, double* __restrict__ out,
+                                  int64_t scal0) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < len; e += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0, c = 0.0;
+    for (int k = 0; k < nch; ++k) {
+      const double v = chunks[(int64_t)k * len + e];
+      if (e >= scal0) neumaier_add(s, c, v);
+      else s += v;
+    }
+    out[e] = s + c;
+  }
+}
+
 // Packed lower triangle (row-major) -> column-major p x p lower triangle (for potrf) and X'Wz.
 __global__ void unpack_lower_kernel(const double* __restrict__ packed, int p, double* __restrict__ A,
                                     double* __restrict__ b) {
@@ -502,6 +549,14 @@ hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(wide_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, stride, st_range, p, rowpart, nrow, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_chunks(const double* chunks, int nch, int p, double* out, hipStream_t st) {
+  const int64_t len = (int64_t)p * (p + 1) / 2 + p + NS;
+  int blocks = (int)((len + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(sum_chunks_kernel, dim3(blocks), dim3(256), 0, st, chunks, nch, len, out, len - NS);
   return hipGetLastError();
 }
 

@@ -1,0 +1,66 @@
+"""HBM bytes per row, clock and MFMA busy of each PMC workload (tools/pmc_workloads.sh output)
+-> the profiles/pmc_traffic.json entries bench.py reads for roofline.traffic.
+
+Method (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE and WRITE_SIZE in separate
+--pmc passes; FETCH_SIZE doubled (gfx950 reports half of a 16-B/lane streaming read); KB x 1024;
+summed over the pass's kernels (narrow / fused: one kernel; wide: row + Gram kernels), per row.
+clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
+(1024 SIMDs x clock cycles).
+usage: python tools/pmc_traffic.py gpurun_out/pmc SOURCE_LABEL [profiles/pmc_traffic.json]"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WL = {  # name: (key, rows, kernel substrings of the pass)
+    "logit32": ("binomial:32", 100_000_000, ["irls_narrow_kernel"]),
+    "poisson64": ("poisson:64", 50_000_000, ["irls_narrow_kernel"]),
+    "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel"]),
+    "logit512": ("binomial:512", 8_000_000, ["wide_rows_kernel", "wide_gram_kernel"]),
+    "logit512p": ("binomial:512:proc", 8_000_000, ["wide_rows_kernel", "wide_gram_kernel"]),
+    "gamma2048": ("gamma:2048", 2_000_000, ["wide_rows_kernel", "wide_gram_kernel"]),
+}
+
+
+def load(d, wl):
+    out = subprocess.run([sys.executable, os.path.join(HERE, "pmc_sum.py")] +
+                         [os.path.join(d, f"{wl}_{i}") for i in (1, 2, 3)] + ["--kernel", "sglm", "--json"],
+                         capture_output=True, text=True, check=True).stdout
+    return json.loads(out)
+
+
+def main():
+    d, label = sys.argv[1], sys.argv[2]
+    path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(HERE), "profiles", "pmc_traffic.json")
+    tab = json.load(open(path)) if os.path.exists(path) else {}
+    for wl, (key, rows, subs) in WL.items():
+        if not os.path.isdir(os.path.join(d, f"{wl}_1")):
+            continue
+        ks = {k: v for k, v in load(d, wl).items() if any(s in k for s in subs)}
+        fetch = sum(v.get("FETCH_SIZE", 0) for v in ks.values()) * 2 * 1024
+        write = sum(v.get("WRITE_SIZE", 0) for v in ks.values()) * 1024
+        ms = sum(v.get("avg_ms") or 0 for v in ks.values())
+        grbm = sum(v.get("GRBM_GUI_ACTIVE", 0) for v in ks.values())
+        mfma = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) for v in ks.values())
+        cyc = grbm / 8
+        entry = {"bytes_per_row": (fetch + write) / rows, "measured_rows": rows, "kernels": sorted(ks),
+                 "fetch_bytes_per_row": fetch / rows, "write_bytes_per_row": write / rows,
+                 "kernel_ms_profiled": ms, "clock_ghz": cyc / (ms * 1e-3) / 1e9 if ms else None,
+                 "mfma_busy_frac": mfma / (1024 * cyc) if cyc else None, "source": label,
+                 "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE / GRBM_GUI_ACTIVE+SQ_VALU_MFMA_BUSY_CYCLES "
+                           "in separate passes over tools/pass_bench.py (tools/pmc_workloads.sh); FETCH_SIZE doubled "
+                           "(gfx950 reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md); KB x 1024; summed "
+                           "over the pass's kernels; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; MFMA busy = "
+                           "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock cycles)"}
+        if key in tab:
+            prev = tab[key]
+            entry["previous"] = {k: prev.get(k) for k in ("bytes_per_row", "clock_ghz", "mfma_busy_frac", "source")}
+        tab[key] = entry
+        print(f"{key:20s} {entry['bytes_per_row']:9.1f} B/row (fetch {entry['fetch_bytes_per_row']:.1f}, write "
+              f"{entry['write_bytes_per_row']:.1f})  clock {entry['clock_ghz']:.2f} GHz  MFMA busy {entry['mfma_busy_frac']:.3f}")
+    json.dump(tab, open(path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -2,9 +2,9 @@
 # PMC evidence per bench workload: HBM bytes (FETCH_SIZE, WRITE_SIZE: separate passes) and
 # clock / MFMA busy, over tools/pass_bench.py at a reduced row count (same per-row pattern).
 cd "$GRAFT_REPO_ROOT" || exit 1
-run_wl() {  # name PN PP PKIND PF PL
+run_wl() {  # name PN PP PKIND PF PL [PPROC]
   local name=$1
-  export PN=$2 PP=$3 PKIND=$4 PF=$5 PL=$6 PK=2
+  export PN=$2 PP=$3 PKIND=$4 PF=$5 PL=$6 PK=2 PPROC=${7:-0}
   bash tools/pmc_counters.sh "$name" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" || exit 1
 }
 for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
@@ -14,6 +14,7 @@ for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
     logit512) run_wl logit512 8000000 512 0 binomial logit ;;
     gamma2048) run_wl gamma2048 2000000 2048 3 gamma inverse ;;
     logit32) run_wl logit32 100000000 32 0 binomial logit ;;   # logit1b's per-row pattern
+    logit512p) run_wl logit512p 8000000 512 0 binomial logit 1 ;;  # procedural shard (HBM-scratch chunks)
   esac
 done
 exit 0

@@ -96,12 +96,15 @@ struct WideRowArgs {
   int64_t xs_ld;        //   leading dimension xs_ld, local row = row - r_begin), else null
 };
 
-// One run of consecutive 16-row blocks of one super-tile, processed by one workgroup of
-// the persistent Gram kernel and written to partial slot `slot`.
+// One run of 16-row blocks of one super-tile, processed by one workgroup of the persistent
+// Gram kernel and written to partial slot `slot`: blocks b0, b0 + bs, b0 + 2 bs, ... < b1
+// (bs = 1: consecutive blocks; bs = k: the k workgroups of a super-tile interleave block by
+// block, so every workgroup of the launch sweeps the same rows at the same time).
 struct WidePiece {
-  int64_t b0, b1;       // [b0, b1) blocks of WIDE_RB rows
+  int64_t b0, b1;       // blocks of WIDE_RB rows
   int st;               // super-tile I(I+1)/2 + J
   int slot;             // partial slot (slots of one super-tile are consecutive)
+  int64_t bs;           // block stride
 };
 constexpr int WIDE_RB = 16;   // rows per Gram-kernel LDS block
 

@@ -293,6 +293,19 @@ struct sglm_engine : public Backend {
   // diagonal / diagonal super-tiles) the (super-tile, block) line, super-tile major, is cut
   // into ggrid equal segments; a segment's runs inside one super-tile are its pieces.
   // Pieces are numbered in line order, so the partial slots of a super-tile are consecutive.
+  //
+  // Banded schedule (wide_band, when ggrid / S workgroups per super-tile leave few idle): the k
+  // workgroups of each super-tile take its blocks round-robin (block stride k), so all S * k
+  // workgroups sweep the rows together and a block read by one super-tile's workgroup is read
+  // by the others' while it is still in the Infinity Cache / L2; the workgroups that read the
+  // same blocks are numbered onto the same XCD (blockIdx % 8).
+  int wide_band = 1;  // SGLM_WIDE_BAND: 0 off, 1 when <= 3 % of the workgroups idle, 2 always
+  bool banded_kind(int S, int64_t nb) const {
+    if (wide_band == 0 || S <= 0 || nb < 2) return false;
+    const int k = ggrid / S;
+    if (k < 2) return false;
+    return wide_band == 2 || (double)(ggrid - k * S) <= 0.03 * ggrid;
+  }
   int build_wide_schedule() {
     const int64_t nb = (nch > 0 ? ch_rows : n_pad) / WIDE_RB;
     std::vector<int> str((size_t)nst * 2, 0);
@@ -307,26 +320,51 @@ struct sglm_engine : public Backend {
       const int64_t total = nb * (int64_t)sts.size();
       std::vector<WidePiece> pieces;
       std::vector<int> wgb((size_t)ggrid + 1, 0);
-      int64_t pos = 0, b = 0;
-      size_t si = 0;
-      for (int g = 0; g < ggrid; ++g) {
-        wgb[(size_t)g] = (int)pieces.size();
-        const int64_t end = (int64_t)((__int128)total * (g + 1) / ggrid);
-        while (si < sts.size() && pos < end) {
-          const int64_t k = std::min(nb - b, end - pos);
-          const int st = sts[si];
-          if (b == 0) str[(size_t)st * 2] = slot;
-          pieces.push_back(WidePiece{b, b + k, st, slot++});
-          str[(size_t)st * 2 + 1] = slot;
-          pos += k;
-          b += k;
-          if (b == nb) {
-            ++si;
-            b = 0;
+      if (banded_kind((int)sts.size(), nb)) {
+        const int S = (int)sts.size();
+        const int k = (int)std::min<int64_t>(ggrid / S, nb);
+        const int per_xcd = std::max(1, ggrid / 8);
+        std::vector<int> owner((size_t)ggrid, -1);  // workgroup -> pair index q = j * S + s
+        for (int q = 0; q < S * k; ++q) {
+          const int g = (ggrid % 8 == 0) ? (q % per_xcd) * 8 + q / per_xcd : q;
+          owner[(size_t)g] = q;
+        }
+        std::vector<int> qslot((size_t)S * k);
+        for (int s = 0; s < S; ++s) {  // slots of one super-tile consecutive, in j order
+          str[(size_t)sts[(size_t)s] * 2] = slot;
+          for (int j = 0; j < k; ++j) qslot[(size_t)j * S + s] = slot++;
+          str[(size_t)sts[(size_t)s] * 2 + 1] = slot;
+        }
+        for (int g = 0; g < ggrid; ++g) {
+          wgb[(size_t)g] = (int)pieces.size();
+          const int q = owner[(size_t)g];
+          if (q < 0) continue;
+          const int j = q / S, s = q % S;
+          pieces.push_back(WidePiece{j, nb, sts[(size_t)s], qslot[(size_t)q], k});
+        }
+        wgb[(size_t)ggrid] = (int)pieces.size();
+      } else {
+        int64_t pos = 0, b = 0;
+        size_t si = 0;
+        for (int g = 0; g < ggrid; ++g) {
+          wgb[(size_t)g] = (int)pieces.size();
+          const int64_t end = (int64_t)((__int128)total * (g + 1) / ggrid);
+          while (si < sts.size() && pos < end) {
+            const int64_t k = std::min(nb - b, end - pos);
+            const int st = sts[si];
+            if (b == 0) str[(size_t)st * 2] = slot;
+            pieces.push_back(WidePiece{b, b + k, st, slot++, 1});
+            str[(size_t)st * 2 + 1] = slot;
+            pos += k;
+            b += k;
+            if (b == nb) {
+              ++si;
+              b = 0;
+            }
           }
         }
+        wgb[(size_t)ggrid] = (int)pieces.size();
       }
-      wgb[(size_t)ggrid] = (int)pieces.size();
       HIPCHK(hipMalloc(&dpieces[kind], sizeof(WidePiece) * pieces.size()));
       HIPCHK(hipMalloc(&dwgb[kind], sizeof(int) * wgb.size()));
       HIPCHK(hipMemcpy(dpieces[kind], pieces.data(), sizeof(WidePiece) * pieces.size(), hipMemcpyHostToDevice));
@@ -1170,6 +1208,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
+  if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
   *out = h;
   return SGLM_OK;
 }

@@ -29,6 +29,9 @@
 #ifndef WIDE_SPREAD_DMA
 #define WIDE_SPREAD_DMA 1
 #endif
+#ifndef WIDE_DIAG2
+#define WIDE_DIAG2 0  // diagonal super-tiles: two blocks per LDS stage / barrier (measured 1 % slower)
+#endif
 
 namespace sglm {
 
@@ -58,8 +61,8 @@ constexpr int WRB = WIDE_RB;               // rows per block (16)
 constexpr int PB = PANEL * WRB;            // doubles per panel block image (2048)
 constexpr int TB = 16 * WRB;               // doubles per 16-column tile block (256)
 constexpr int OFF_X = 0;                   // [2 buffers][2 panels (I, J)][PB]
-constexpr int OFF_V = 4 * PB;              // [2 buffers][w, w*z][WRB]
-constexpr int LDS_DOUBLES = OFF_V + 4 * WRB;
+constexpr int OFF_V = 4 * PB;              // [2 buffers][2 slots][w, w*z][WRB]
+constexpr int LDS_DOUBLES = OFF_V + 8 * WRB;
 constexpr int NWAVE = 4;                   // one wave per SIMD; two workgroups per CU
 
 __device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
@@ -98,7 +101,41 @@ __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs&
     const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
     const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
     if (lane < WRB / 2)
-      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 4 + v) * WRB), 16, 0, 0);
+  }
+}
+
+// Diagonal super-tiles stage TWO blocks per buffer (slot 0 and slot 1 of the panel images the
+// off-diagonal kernel uses for panels I and J), so each barrier covers 2 x 36 MFMAs per wave.
+// This call stages block blk of panel I into slot sl: four octets per wave, and w (waves
+// 2 sl) / w*z (wave 2 sl + 1) of the block.
+template <bool PROC>
+__device__ __forceinline__ void wstage_diag(double* lds, int buf, int sl, const WideGramArgs& a, int64_t blk, int I,
+                                            int wv, const int64_t (&loff)[2], int lane) {
+  const double* xb = a.X + blk * WRB;
+  double* dst = lds + OFF_X + (buf * 2 + sl) * PB;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ol = wv * 4 + k;
+    const int c0 = I * PANEL + ol * 8;
+    if (c0 < a.ncols) {
+      if constexpr (PROC) {
+        const int oc = lane >> 3, i = lane & 7;
+        const int64_t r = blk * WRB + ((2 * i) ^ swz(8 * (ol & 1) + oc));
+        const double2 v = {proc_x(a.proc, r, c0 + oc), proc_x(a.proc, r + 1, c0 + oc)};
+        *(double2*)(dst + ol * 128 + 2 * lane) = v;
+      } else {
+        __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
+                                         (lds_void*)(dst + ol * 128), 16, 0, 0);
+      }
+    }
+  }
+  if ((wv >> 1) == sl) {
+    const int v = wv & 1;
+    const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
+    if (lane < WRB / 2)
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + ((buf * 2 + sl) * 2 + v) * WRB),
+                                       16, 0, 0);
   }
 }
 
@@ -122,7 +159,7 @@ __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv
   const int f = 2 * (cl >> 1);
   const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB + TB * (4 * (wv >> 1));
   const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * WRB + TB * (4 * (wv & 1));
-  const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
+  const double* w = lds + OFF_V + (buf * 4 + 0) * WRB;
   double av[2][4], bv[2][4], wr[2];
   auto load = [&](int s, int slot) {
     const int r = 4 * s + rq;
@@ -153,28 +190,37 @@ __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv
 // Diagonal super-tile: wave q owns tile rows LO = q and HI = 7-q of the lower tile grid,
 // tiles (LO,0..LO) and (HI,0..HI): 9 tiles, 36 over the four waves; X'Wz on the VALU.
 template <int Q>
-__device__ __forceinline__ void diag_block(const double* lds, int buf, int lane, d4 (&acc)[9], double& xz_lo,
+__device__ __forceinline__ void diag_block(const double* lds, int buf, int sl, int lane, d4 (&acc)[9], double& xz_lo,
                                            double& xz_hi) {
-  constexpr int LO = Q, HI = PT - 1 - Q;
+  constexpr int LO = Q, HI = PT - 1 - Q;  // HI >= LO: the B operands are tile columns 0..HI
   const int cl = lane & 15, rq = lane >> 4;
   const int f = 2 * (cl >> 1);
-  const double* xs = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB;
-  const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
-  const double* wz = lds + OFF_V + (buf * 2 + 1) * WRB;
-#pragma unroll
-  for (int s = 0; s < WRB / 4; ++s) {
+  const double* xs = lds + OFF_X + (buf * 2 + sl) * PB + cl * WRB;
+  const double* w = lds + OFF_V + ((buf * 2 + sl) * 2 + 0) * WRB;
+  const double* wz = lds + OFF_V + ((buf * 2 + sl) * 2 + 1) * WRB;
+  // operands of k-step s + 1 are read from LDS while the 9 MFMAs of step s issue
+  double xv[2][HI + 1], wr[2], wzr[2];
+  auto load = [&](int s, int slot) {
     const int r = 4 * s + rq;
     const int o = r ^ f;
-    const double wr = w[r], wzr = wz[r];
-    const double x_lo = xs[o + TB * LO], x_hi = xs[o + TB * HI];
-    const double a_lo = x_lo * wr, a_hi = x_hi * wr;
-    xz_lo += x_lo * wzr;
-    xz_hi += x_hi * wzr;
+    wr[slot] = w[r];
+    wzr[slot] = wz[r];
 #pragma unroll
-    for (int k = 0; k <= PT; ++k) {
-      const double b = xs[o + TB * (k <= LO ? k : k - LO - 1)];
-      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
-    }
+    for (int c = 0; c <= HI; ++c) xv[slot][c] = xs[o + TB * c];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int s = 0; s < WRB / 4; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < WRB / 4) load(s + 1, cur ^ 1);
+    const double x_lo = xv[cur][LO], x_hi = xv[cur][HI];
+    const double a_lo = x_lo * wr[cur], a_hi = x_hi * wr[cur];
+    xz_lo += x_lo * wzr[cur];
+    xz_hi += x_hi * wzr[cur];
+#pragma unroll
+    for (int k = 0; k <= PT; ++k)
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, xv[cur][k <= LO ? k : k - LO - 1], acc[k],
+                                                    0, 0, 0);
   }
 }
 
@@ -184,22 +230,40 @@ __device__ __forceinline__ void diag_block(const double* lds, int buf, int lane,
 //   MFMAs of block blk.  The DMA of blk+1 flies under blk's MFMAs, and the second
 //   workgroup on the CU covers whatever latency is left.
 template <int Q, bool PROC>
-__device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int wv, int lane,
-                           double* out) {
+__device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0, int64_t b1, int64_t bs, int wv,
+                           int lane, double* out) {
   d4 acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
   double xz_lo = 0.0, xz_hi = 0.0;
   int64_t loff[2];
   lane_offsets(a, lane, loff);
-  wstage<true, PROC>(lds, 0, a, b0, I, I, wv, loff, lane);
+  int cur = 0;
+  if constexpr (!WIDE_DIAG2) {
+    wstage_diag<PROC>(lds, 0, 0, a, b0, I, wv, loff, lane);
 #pragma unroll 1
-  for (int64_t blk = b0; blk < b1; ++blk) {
-    const int cur = (int)((blk - b0) & 1);
-    wait_vm<0>();
-    lds_bar();
-    if (blk + 1 < b1) wstage<true, PROC>(lds, cur ^ 1, a, blk + 1, I, I, wv, loff, lane);
-    diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
+    for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
+      wait_vm<0>();
+      lds_bar();
+      if (blk + bs < b1) {
+        wstage_diag<PROC>(lds, cur ^ 1, 0, a, blk + bs, I, wv, loff, lane);
+      }
+      diag_block<Q>(lds, cur, 0, lane, acc, xz_lo, xz_hi);
+    }
+  }
+  if constexpr (WIDE_DIAG2) {
+    wstage_diag<PROC>(lds, 0, 0, a, b0, I, wv, loff, lane);
+    if (b0 + bs < b1) wstage_diag<PROC>(lds, 0, 1, a, b0 + bs, I, wv, loff, lane);
+#pragma unroll 1
+    for (int64_t blk = b0; blk < b1; blk += 2 * bs, cur ^= 1) {
+      const int64_t nb = blk + 2 * bs;
+      wait_vm<0>();
+      lds_bar();
+      if (nb < b1) wstage_diag<PROC>(lds, cur ^ 1, 0, a, nb, I, wv, loff, lane);
+      if (nb + bs < b1) wstage_diag<PROC>(lds, cur ^ 1, 1, a, nb + bs, I, wv, loff, lane);
+      diag_block<Q>(lds, cur, 0, lane, acc, xz_lo, xz_hi);
+      if (blk + bs < b1) diag_block<Q>(lds, cur, 1, lane, acc, xz_lo, xz_hi);
+    }
   }
   constexpr int LO = Q, HI = PT - 1 - Q;
 #pragma unroll
@@ -220,8 +284,8 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
 }
 
 template <bool PROC>
-__device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int wv,
-                              int lane, double* out) {
+__device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, int64_t b0, int64_t b1, int64_t bs,
+                              int wv, int lane, double* out) {
   d4 acc[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
@@ -229,30 +293,31 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
+  int cur = 0;
 #pragma unroll 1
-  for (int64_t blk = b0; blk < b1; ++blk) {
-    const int cur = (int)((blk - b0) & 1);
+  for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
+    const int64_t nb = blk + bs;
     wait_vm<0>();
     if (!(dbg & 32)) lds_bar();
-    const bool next = blk + 1 < b1 && (!(dbg & 4) || blk == b0);
+    const bool next = nb < b1 && (!(dbg & 4) || blk == b0);
     if constexpr (PROC) {  // generate block blk+1 two octets per k-step, under the MFMAs
       offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
         if (!next) return;
-        if (s == 0) wstage<false, true, 0, 2>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 1) wstage<false, true, 2, 4>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 2) wstage<false, true, 4, 6>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 3) wstage<false, true, 6, 8>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 0) wstage<false, true, 0, 2>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 1) wstage<false, true, 2, 4>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 2) wstage<false, true, 4, 6>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 3) wstage<false, true, 6, 8>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
       });
     } else if (WIDE_SPREAD_DMA) {  // issue block blk+1's DMA two octets per k-step, under the MFMAs
       offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
         if (!next) return;
-        if (s == 0) wstage<false, false, 0, 2>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 1) wstage<false, false, 2, 4>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 2) wstage<false, false, 4, 6>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
-        if (s == 3) wstage<false, false, 6, 8>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+        if (s == 0) wstage<false, false, 0, 2>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 1) wstage<false, false, 2, 4>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 2) wstage<false, false, 4, 6>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
+        if (s == 3) wstage<false, false, 6, 8>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
       });
     } else {
-      if (next) wstage<false, false>(lds, cur ^ 1, a, blk + 1, I, J, wv, loff, lane);
+      if (next) wstage<false, false>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
       offdiag_block(lds, cur, wv, lane, acc, [](int) {});
     }
   }
@@ -287,13 +352,13 @@ __global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a
     const int J = st - I * (I + 1) / 2;
     double* out = a.partials + (int64_t)pz.slot * a.stride;
     if constexpr (!DIAG) {
-      offdiag_piece<PROC>(lds, a, I, J, pz.b0, pz.b1, wv, lane, out);
+      offdiag_piece<PROC>(lds, a, I, J, pz.b0, pz.b1, pz.bs, wv, lane, out);
     } else {
       switch (wv) {
-        case 0: diag_piece<0, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        case 1: diag_piece<1, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        case 2: diag_piece<2, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
-        default: diag_piece<3, PROC>(lds, a, I, pz.b0, pz.b1, wv, lane, out); break;
+        case 0: diag_piece<0, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
+        case 1: diag_piece<1, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
+        case 2: diag_piece<2, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
+        default: diag_piece<3, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
       }
     }
     lds_bar();  // every wave is done with both buffers before the next piece stages

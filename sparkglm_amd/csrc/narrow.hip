@@ -76,6 +76,14 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef SGLM_NBATCH
 #define SGLM_NBATCH 0
 #endif
+// Row pairs (NRB = 32, p <= 32): the family arithmetic runs on 32 of the wave's 64 lanes, so
+// blocks are taken in pairs -- the first block's eta, row values and Gram operands are stashed
+// in registers and its buffer released at once; with the second block, the family arithmetic
+// covers both blocks' rows on all 64 lanes (upper half: the stashed block), then both blocks'
+// MFMAs run from registers.  Half the family-arithmetic instructions per row.
+#ifndef SGLM_NPAIR
+#define SGLM_NPAIR 1
+#endif
 constexpr int NPRIO = SGLM_NPRIO;
 
 // Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
@@ -106,8 +114,9 @@ struct NGeo {
   static constexpr int BSTR = 16 * NRB + 2;         // (+2: keeps LDS-DMA destinations 16-B aligned)
   static constexpr int XB = P16 * BSTR;              // doubles of X per buffer
   static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
-  static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB]
-  static constexpr int WAVE_LDS = OFF_W + 2 * NRB;   // doubles per wave
+  static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB] (PAIR: w[2 NRB], w*z[2 NRB])
+  static constexpr bool PAIR = SGLM_NPAIR && NRB == 32;
+  static constexpr int WAVE_LDS = OFF_W + (PAIR ? 4 : 2) * NRB;  // doubles per wave
   static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
   static_assert(NW % 4 == 0, "whole waves per SIMD");
@@ -247,6 +256,110 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
   if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
 
+  if constexpr (G::PAIR) {
+    constexpr int KS = NRB / 4;
+    double xp[KS][P16];  // the stashed block's Gram operands (lane (rq, cl): row 4s + rq, column 16b + cl)
+    double eta_p = 0.0, y_p = 0.0, m_p = 1.0, off_p = 0.0, pw_p = 1.0;
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int b = 0; b < P16; ++b) xp[k][b] = 0.0;
+#pragma unroll 1
+    for (int64_t blk = b0; blk < b1; ++blk) {
+      const int buf = (int)((blk - b0) & 1);
+      const bool second = ((blk - b0) & 1) != 0;     // uniform
+      const bool single = !second && blk + 1 >= b1;  // the range's last block has no partner
+      if (NPRIO > 0) {
+        if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+      // block blk landed; block blk+1 may still fly, and after a pair's second block its eta store
+      if (blk + 1 >= b1) wait_vm<0>();
+      else if (has_eta && !second && blk > b0) wait_vm<G::NOCT + 2>();
+      else wait_vm<G::NOCT + 1>();
+      const double* xs = wl + buf * G::BUF;
+      const double* vv = xs + G::XB;
+      double eta = 0.0;
+      if (irls && !(SGLM_DBG(a) & 8)) {
+        double e4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+          const int c = LPR * u + g;
+          e4[u & 3] += xs[(c >> 4) * G::BSTR + (c & 15) * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
+        }
+        eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+        eta = xor32_sum(eta);  // LPR == 2: both halves hold row rl's eta
+      }
+      const double yv = vv[rl];
+      const double mv = a.m ? vv[NRB + rl] : 1.0;
+      const double ov = a.off ? vv[2 * NRB + rl] : 0.0;
+      const double pv = a.prior ? vv[3 * NRB + rl] : 1.0;
+      if (irls) eta = eta + ov;
+      if (!second && !single) {
+        // first block of a pair: stash, release the buffer
+        eta_p = eta;
+        y_p = yv;
+        m_p = mv;
+        off_p = ov;
+        pw_p = pv;
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int b = 0; b < P16; ++b) xp[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+        continue;
+      }
+      // family arithmetic: lanes [0, 32) this block's row rl, lanes [32, 64) the stashed block's
+      const bool hi = lane >= NRB;
+      const int64_t row = hi ? (blk - 1) * NRB + rl : blk * NRB + rl;
+      double w = 0.0, wz = 0.0;
+      if (!(single && hi)) {
+        const double et = hi ? eta_p : eta;
+        if (irls && has_eta) a.eta_out[row] = et;
+        if (row < a.n && do_rows) {
+          const double y = hi ? y_p : yv, m = hi ? m_p : mv, off = hi ? off_p : ov, pw = hi ? pw_p : pv;
+          if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = et * w; s_dev += w; }
+          else if constexpr (STATS)
+            pass_row_logit_stats(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
+          else
+            pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
+                     !IRLS);
+        }
+      }
+      // w / w*z at [half * NRB + rl]: the stashed block in the upper half
+      wl[G::OFF_W + lane] = w;
+      wl[G::OFF_W + 2 * NRB + lane] = wz;
+      // this block's Gram operands into registers, then release the buffer
+      double xc[KS][P16];
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int b = 0; b < P16; ++b) xc[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+      if (do_gram) {
+        // rows in order: the stashed block (upper-half w), then this one
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h == 0 && single) continue;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) {
+            const int r = 4 * k + rq + (h == 0 ? NRB : 0);
+            const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + 2 * NRB + r];
+            double av[P16], xk[P16], d1[P16], d2[P16];
+#pragma unroll
+            for (int b = 0; b < P16; ++b) {
+              xk[b] = h == 0 ? xp[k][b] : xc[k][b];
+              av[b] = xk[b] * wr;
+              xz[b] += xk[b] * wzr;
+            }
+            gram_kstep<P16>(acc, av, xk, d1, d2);
+          }
+        }
+      }
+    }
+  } else {
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; ++blk) {
     const int buf = (int)((blk - b0) & 1);
@@ -441,6 +554,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     NSTAMP(4);
   }
 #endif
+  }  // !PAIR
 
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
 #pragma unroll

@@ -68,6 +68,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 // computes the upper half.  Measured (tools/ab_narrow2.sh, round 2): correct, but p = 32
 // +1 % and p = 64 +39 % per pass -- the 4x4x4 accumulation chains and the extra rotated-operand
 // LDS reads cost more than the 25 % of diagonal-tile MFMA cycles they save.  Off by default.
+// SGLM_NDIAG44 = 2: the same in the row-pair loop only (p <= 32), with the rotated B operands
+// formed from the registers by DPP row rotations instead of LDS reads.
 #ifndef SGLM_NDIAG44
 #define SGLM_NDIAG44 0
 #endif
@@ -116,6 +118,7 @@ struct NGeo {
   static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
   static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB] (PAIR: w[2 NRB], w*z[2 NRB])
   static constexpr bool PAIR = SGLM_NPAIR && NRB == 32;
+  static constexpr bool D44 = PAIR ? SGLM_NDIAG44 != 0 : SGLM_NDIAG44 == 1;  // diagonal tiles on 4x4x4
   static constexpr int WAVE_LDS = OFF_W + (PAIR ? 4 : 2) * NRB;  // doubles per wave
   static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
@@ -142,6 +145,16 @@ __device__ __forceinline__ double xor32_sum(double v) {
   const auto a = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
   const auto b = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
   return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
+// v within each 16-lane row rotated so that lane 16 q + c reads lane 16 q + ((c + R) & 15):
+// DPP row_ror:(16 - R) on both halves of the double.
+template <int R>
+__device__ __forceinline__ double row_rot(double v) {
+  constexpr int ctrl = 0x120 + ((16 - R) & 15);  // row_ror
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
 
 // DMA of block blk into buffer buf of this wave's image: NOCT wave-instructions of CPI
@@ -171,7 +184,7 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
 // the tile's columns (lane 16k + 4 blk + m: row k, column 4 blk + m -- the 16x16x4 A layout),
 // the B operand rotated by rr groups of 4 lanes (column 4 ((blk + rr) & 3) + n) gives block blk
 // the 4x4 sub-block (blk, (blk + rr) & 3) of the tile in lane 16 m + 4 blk + n.
-template <int P16>
+template <int P16, bool D44 = NGeo<P16>::D44>
 __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double (&av)[P16], const double (&xv)[P16],
                                            const double (&x1)[P16], const double (&x2)[P16]) {
   int t = 0;
@@ -179,7 +192,7 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
   for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
     for (int bj = 0; bj <= bi; ++bj, ++t) {
-      if (SGLM_NDIAG44 && bi == bj) {
+      if (D44 && bi == bj) {
         acc[t][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], xv[bi], acc[t][0], 0, 0, 0);
         acc[t][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x1[bi], acc[t][1], 0, 0, 0);
         acc[t][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x2[bi], acc[t][2], 0, 0, 0);
@@ -353,6 +366,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
               xk[b] = h == 0 ? xp[k][b] : xc[k][b];
               av[b] = xk[b] * wr;
               xz[b] += xk[b] * wzr;
+              if constexpr (G::D44) {  // columns 4 and 8 on within the 16-column block
+                d1[b] = row_rot<4>(xk[b]);
+                d2[b] = row_rot<8>(xk[b]);
+              }
             }
             gram_kstep<P16>(acc, av, xk, d1, d2);
           }
@@ -475,7 +492,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
           xv[b] = base[G::BSTR * b];
-          if (SGLM_NDIAG44) {
+          if (G::D44) {
             x1[b] = base1[G::BSTR * b];
             x2[b] = base2[G::BSTR * b];
           }
@@ -499,7 +516,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
           xv[b] = base[G::BSTR * b];
-          if (SGLM_NDIAG44) {
+          if (G::D44) {
             x1[b] = base1[G::BSTR * b];
             x2[b] = base2[G::BSTR * b];
           }
@@ -518,7 +535,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
           for (int b = 0; b < P16; ++b) {
             xn[b] = base[G::BSTR * b];
-            if (SGLM_NDIAG44) {
+            if (G::D44) {
               xn1[b] = base1[G::BSTR * b];
               xn2[b] = base2[G::BSTR * b];
             }
@@ -537,7 +554,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
           for (int b = 0; b < P16; ++b) {
             xv[b] = xn[b];
-            if (SGLM_NDIAG44) {
+            if (G::D44) {
               x1[b] = xn1[b];
               x2[b] = xn2[b];
             }
@@ -622,7 +639,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
       for (int bj = 0; bj <= bi; ++bj, ++t) {
-        if (SGLM_NDIAG44 && bi == bj) {
+        if (G::D44 && bi == bj) {
           // 4x4x4 layout -> tile element (i, j) at 16 i + j (reduce_partials_kernel reads i >= j):
           // rotation rr, lane 16 m + 4 blk + n holds sub-block (blk, J = (blk + rr) & 3), element
           // (4 blk + m, 4 J + n); an upper sub-block (blk < J) is stored transposed (the tile is

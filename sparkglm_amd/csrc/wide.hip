@@ -49,7 +49,8 @@ __device__ __forceinline__ void wait_vm() {
 
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// LDS image (doubles) of one 16-row block of one 128-column panel: column c at c*16, row r
+// LDS image (doubles) of one 16-row block of one 128-column panel: column c at (c >> 4) TB +
+// 16 (c & 15), row r
 // in slot r ^ f(c), f(c) = 2((c >> 1) & 7).  The XOR is applied on the DMA source address
 // (the LDS-DMA destination is lane-linear; f even keeps each lane's 16-byte row pair
 // contiguous) and makes the MFMA fragment reads (ds_read_b64, lanes (rq, cl) reading row
@@ -58,8 +59,13 @@ __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n
 constexpr int PANEL = WIDE_PANEL;          // columns per panel
 constexpr int PT = PANEL / 16;             // 16-column tile blocks per panel (8)
 constexpr int WRB = WIDE_RB;               // rows per block (16)
-constexpr int PB = PANEL * WRB;            // doubles per panel block image (2048)
-constexpr int TB = 16 * WRB;               // doubles per 16-column tile block (256)
+// 16-column tile blocks TB = 16 WRB + 2 doubles apart: the pad keeps the MFMA operand reads of
+// the four tiles of a wave row plain ds_read_b64 -- at 256 doubles apart the compiler pairs them
+// into ds_read2st64_b64 (8 LDS cycles, and 2-way bank conflicts under the row swizzle: PMC
+// SQ_LDS_BANK_CONFLICT was 48 % of the Gram kernels' LDS cycles).  (+2 keeps the LDS-DMA
+// destinations 16-byte aligned.)
+constexpr int TB = 16 * WRB + 2;           // doubles per 16-column tile block, padded (258)
+constexpr int PB = PT * TB;                // doubles per panel block image (2064)
 constexpr int OFF_X = 0;                   // [2 buffers][2 panels (I, J)][PB]
 constexpr int OFF_V = 4 * PB;              // [2 buffers][2 slots][w, w*z][WRB]
 constexpr int LDS_DOUBLES = OFF_V + 8 * WRB;
@@ -90,10 +96,10 @@ __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs&
         const int oc = lane >> 3, i = lane & 7;
         const int64_t r = blk * WRB + ((2 * i) ^ swz(8 * (ol & 1) + oc));
         const double2 v = {proc_x(a.proc, r, c0 + oc), proc_x(a.proc, r + 1, c0 + oc)};
-        *(double2*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128 + 2 * lane) = v;
+        *(double2*)(lds + OFF_X + (buf * 2 + ps) * PB + (ol >> 1) * TB + (ol & 1) * 128 + 2 * lane) = v;
       } else {
         __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
-                                         (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + ol * 128), 16, 0, 0);
+                                         (lds_void*)(lds + OFF_X + (buf * 2 + ps) * PB + (ol >> 1) * TB + (ol & 1) * 128), 16, 0, 0);
       }
     }
   }
@@ -123,10 +129,10 @@ __device__ __forceinline__ void wstage_diag(double* lds, int buf, int sl, const 
         const int oc = lane >> 3, i = lane & 7;
         const int64_t r = blk * WRB + ((2 * i) ^ swz(8 * (ol & 1) + oc));
         const double2 v = {proc_x(a.proc, r, c0 + oc), proc_x(a.proc, r + 1, c0 + oc)};
-        *(double2*)(dst + ol * 128 + 2 * lane) = v;
+        *(double2*)(dst + (ol >> 1) * TB + (ol & 1) * 128 + 2 * lane) = v;
       } else {
         __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)c0 * a.ld + loff[ol & 1]),
-                                         (lds_void*)(dst + ol * 128), 16, 0, 0);
+                                         (lds_void*)(dst + (ol >> 1) * TB + (ol & 1) * 128), 16, 0, 0);
       }
     }
   }

@@ -294,17 +294,17 @@ struct sglm_engine : public Backend {
   // into ggrid equal segments; a segment's runs inside one super-tile are its pieces.
   // Pieces are numbered in line order, so the partial slots of a super-tile are consecutive.
   //
-  // Banded schedule (wide_band, when ggrid / S workgroups per super-tile leave few idle): the k
-  // workgroups of each super-tile take its blocks round-robin (block stride k), so all S * k
-  // workgroups sweep the rows together and a block read by one super-tile's workgroup is read
-  // by the others' while it is still in the Infinity Cache / L2; the workgroups that read the
-  // same blocks are numbered onto the same XCD (blockIdx % 8).
-  int wide_band = 1;  // SGLM_WIDE_BAND: 0 off, 1 when <= 3 % of the workgroups idle, 2 always
+  // Banded schedule (wide_band): the k = ggrid / S workgroups of each of the S super-tiles take
+  // its blocks round-robin (block stride k), so all S k workgroups sweep the rows together and a
+  // block read by one super-tile's workgroup is read by the others' while it is still in the
+  // Infinity Cache / L2 (the workgroups that read the same blocks are numbered onto the same XCD,
+  // blockIdx % 8).  The E = ggrid - S k workgroups left over take the rows' tail, a fraction
+  // E / ggrid of every super-tile's blocks cut into E equal contiguous segments, so no workgroup
+  // idles and each carries the same work.  Slots of a super-tile: its k strided pieces, then its
+  // tail pieces in row order (the fixed reduction order).
+  int wide_band = 1;  // SGLM_WIDE_BAND: 0 contiguous cost-balanced pieces, 1 banded
   bool banded_kind(int S, int64_t nb) const {
-    if (wide_band == 0 || S <= 0 || nb < 2) return false;
-    const int k = ggrid / S;
-    if (k < 2) return false;
-    return wide_band == 2 || (double)(ggrid - k * S) <= 0.03 * ggrid;
+    return wide_band != 0 && S > 0 && ggrid / S >= 2 && nb >= 2;
   }
   int build_wide_schedule() {
     const int64_t nb = (nch > 0 ? ch_rows : n_pad) / WIDE_RB;
@@ -322,25 +322,44 @@ struct sglm_engine : public Backend {
       std::vector<int> wgb((size_t)ggrid + 1, 0);
       if (banded_kind((int)sts.size(), nb)) {
         const int S = (int)sts.size();
-        const int k = (int)std::min<int64_t>(ggrid / S, nb);
+        const int k = ggrid / S, E = ggrid - S * k;
+        const int64_t tail = nb * E / ggrid, nbm = nb - tail;  // banded blocks [0, nbm), tail [nbm, nb)
         const int per_xcd = std::max(1, ggrid / 8);
-        std::vector<int> owner((size_t)ggrid, -1);  // workgroup -> pair index q = j * S + s
+        std::vector<int> gq((size_t)S * k), extra;  // pair q = j S + s -> workgroup; the left-over workgroups
+        std::vector<char> used((size_t)ggrid, 0);
         for (int q = 0; q < S * k; ++q) {
           const int g = (ggrid % 8 == 0) ? (q % per_xcd) * 8 + q / per_xcd : q;
-          owner[(size_t)g] = q;
+          gq[(size_t)q] = g;
+          used[(size_t)g] = 1;
         }
-        std::vector<int> qslot((size_t)S * k);
-        for (int s = 0; s < S; ++s) {  // slots of one super-tile consecutive, in j order
-          str[(size_t)sts[(size_t)s] * 2] = slot;
-          for (int j = 0; j < k; ++j) qslot[(size_t)j * S + s] = slot++;
-          str[(size_t)sts[(size_t)s] * 2 + 1] = slot;
+        for (int g = 0; g < ggrid; ++g)
+          if (!used[(size_t)g]) extra.push_back(g);
+        struct Pc { int g; int64_t b0, b1, bs; };
+        std::vector<std::vector<Pc>> per_st((size_t)S);
+        for (int j = 0; j < k; ++j)
+          for (int s2 = 0; s2 < S; ++s2)
+            if (j < nbm) per_st[(size_t)s2].push_back(Pc{gq[(size_t)j * S + s2], j, nbm, k});
+        const int64_t tl = (int64_t)S * tail;  // tail line, super-tile major
+        for (int e = 0; e < E && tl > 0; ++e) {
+          int64_t pos = tl * e / E;
+          const int64_t end = tl * (e + 1) / E;
+          while (pos < end) {
+            const int s2 = (int)(pos / tail);
+            const int64_t b = pos % tail, len = std::min(tail - b, end - pos);
+            per_st[(size_t)s2].push_back(Pc{extra[(size_t)e], nbm + b, nbm + b + len, 1});
+            pos += len;
+          }
+        }
+        std::vector<std::vector<WidePiece>> per_g((size_t)ggrid);
+        for (int s2 = 0; s2 < S; ++s2) {
+          const int st = sts[(size_t)s2];
+          str[(size_t)st * 2] = slot;
+          for (const Pc& c : per_st[(size_t)s2]) per_g[(size_t)c.g].push_back(WidePiece{c.b0, c.b1, st, slot++, c.bs});
+          str[(size_t)st * 2 + 1] = slot;
         }
         for (int g = 0; g < ggrid; ++g) {
           wgb[(size_t)g] = (int)pieces.size();
-          const int q = owner[(size_t)g];
-          if (q < 0) continue;
-          const int j = q / S, s = q % S;
-          pieces.push_back(WidePiece{j, nb, sts[(size_t)s], qslot[(size_t)q], k});
+          for (const WidePiece& w : per_g[(size_t)g]) pieces.push_back(w);
         }
         wgb[(size_t)ggrid] = (int)pieces.size();
       } else {

@@ -138,6 +138,7 @@ struct sglm_engine : public Backend {
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
   int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
+  int ggk[2] = {0, 0};  // persistent grid of the off-diagonal / diagonal Gram kernels
   WidePiece* dpieces[2] = {nullptr, nullptr};  // [0] off-diagonal, [1] diagonal super-tiles
   int* dwgb[2] = {nullptr, nullptr};
   int* dstr = nullptr;                          // [nst][2] partial slot range per super-tile
@@ -303,9 +304,7 @@ struct sglm_engine : public Backend {
   // idles and each carries the same work.  Slots of a super-tile: its k strided pieces, then its
   // tail pieces in row order (the fixed reduction order).
   int wide_band = 1;  // SGLM_WIDE_BAND: 0 contiguous cost-balanced pieces, 1 banded
-  bool banded_kind(int S, int64_t nb) const {
-    return wide_band != 0 && S > 0 && ggrid / S >= 2 && nb >= 2;
-  }
+  bool banded_kind(int S, int64_t nb, int G) const { return wide_band != 0 && S > 0 && G / S >= 2 && nb >= 2; }
   int build_wide_schedule() {
     const int64_t nb = (nch > 0 ? ch_rows : n_pad) / WIDE_RB;
     std::vector<int> str((size_t)nst * 2, 0);
@@ -317,22 +316,23 @@ struct sglm_engine : public Backend {
         for (int J = 0; J <= I; ++J)
           if ((I == J) == (kind == 1)) sts.push_back(I * (I + 1) / 2 + J);
       if (sts.empty()) continue;
+      const int G = ggk[kind];
       const int64_t total = nb * (int64_t)sts.size();
       std::vector<WidePiece> pieces;
-      std::vector<int> wgb((size_t)ggrid + 1, 0);
-      if (banded_kind((int)sts.size(), nb)) {
+      std::vector<int> wgb((size_t)G + 1, 0);
+      if (banded_kind((int)sts.size(), nb, G)) {
         const int S = (int)sts.size();
-        const int k = ggrid / S, E = ggrid - S * k;
-        const int64_t tail = nb * E / ggrid, nbm = nb - tail;  // banded blocks [0, nbm), tail [nbm, nb)
-        const int per_xcd = std::max(1, ggrid / 8);
+        const int k = G / S, E = G - S * k;
+        const int64_t tail = nb * E / G, nbm = nb - tail;  // banded blocks [0, nbm), tail [nbm, nb)
+        const int per_xcd = std::max(1, G / 8);
         std::vector<int> gq((size_t)S * k), extra;  // pair q = j S + s -> workgroup; the left-over workgroups
-        std::vector<char> used((size_t)ggrid, 0);
+        std::vector<char> used((size_t)G, 0);
         for (int q = 0; q < S * k; ++q) {
-          const int g = (ggrid % 8 == 0) ? (q % per_xcd) * 8 + q / per_xcd : q;
+          const int g = (G % 8 == 0) ? (q % per_xcd) * 8 + q / per_xcd : q;
           gq[(size_t)q] = g;
           used[(size_t)g] = 1;
         }
-        for (int g = 0; g < ggrid; ++g)
+        for (int g = 0; g < G; ++g)
           if (!used[(size_t)g]) extra.push_back(g);
         struct Pc { int g; int64_t b0, b1, bs; };
         std::vector<std::vector<Pc>> per_st((size_t)S);
@@ -350,24 +350,24 @@ struct sglm_engine : public Backend {
             pos += len;
           }
         }
-        std::vector<std::vector<WidePiece>> per_g((size_t)ggrid);
+        std::vector<std::vector<WidePiece>> per_g((size_t)G);
         for (int s2 = 0; s2 < S; ++s2) {
           const int st = sts[(size_t)s2];
           str[(size_t)st * 2] = slot;
           for (const Pc& c : per_st[(size_t)s2]) per_g[(size_t)c.g].push_back(WidePiece{c.b0, c.b1, st, slot++, c.bs});
           str[(size_t)st * 2 + 1] = slot;
         }
-        for (int g = 0; g < ggrid; ++g) {
+        for (int g = 0; g < G; ++g) {
           wgb[(size_t)g] = (int)pieces.size();
           for (const WidePiece& w : per_g[(size_t)g]) pieces.push_back(w);
         }
-        wgb[(size_t)ggrid] = (int)pieces.size();
+        wgb[(size_t)G] = (int)pieces.size();
       } else {
         int64_t pos = 0, b = 0;
         size_t si = 0;
-        for (int g = 0; g < ggrid; ++g) {
+        for (int g = 0; g < G; ++g) {
           wgb[(size_t)g] = (int)pieces.size();
-          const int64_t end = (int64_t)((__int128)total * (g + 1) / ggrid);
+          const int64_t end = (int64_t)((__int128)total * (g + 1) / G);
           while (si < sts.size() && pos < end) {
             const int64_t k = std::min(nb - b, end - pos);
             const int st = sts[si];
@@ -382,7 +382,7 @@ struct sglm_engine : public Backend {
             }
           }
         }
-        wgb[(size_t)ggrid] = (int)pieces.size();
+        wgb[(size_t)G] = (int)pieces.size();
       }
       HIPCHK(hipMalloc(&dpieces[kind], sizeof(WidePiece) * pieces.size()));
       HIPCHK(hipMalloc(&dwgb[kind], sizeof(int) * wgb.size()));
@@ -400,7 +400,9 @@ struct sglm_engine : public Backend {
     npan = wide_panels((int)p);
     nst = npan * (npan + 1) / 2;
     wstride = wide_stride();
-    ggrid = ncu * wide_gram_wg_per_cu();
+    ggk[0] = ncu * wide_gram_wg_per_cu(false);
+    ggk[1] = ncu * wide_gram_wg_per_cu(true);
+    ggrid = ggk[0];
     int rc = build_wide_schedule();
     if (rc) return rc;
     grid = nslots;
@@ -843,7 +845,7 @@ struct sglm_engine : public Backend {
             if (!has_sched[kind]) continue;
             g.pieces = dpieces[kind];
             g.wg_begin = dwgb[kind];
-            HIPCHK(launch_wide_gram(g, kind == 1, ggrid, st));
+            HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
           }
           HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dchunks + (int64_t)c * plen, st));
         }
@@ -859,7 +861,7 @@ struct sglm_engine : public Backend {
         if (!has_sched[kind]) continue;
         g.pieces = dpieces[kind];
         g.wg_begin = dwgb[kind];
-        HIPCHK(launch_wide_gram(g, kind == 1, ggrid, st));
+        HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
       }
       HIPCHK(hipEventRecord(ev1, st));
       HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dred, st));

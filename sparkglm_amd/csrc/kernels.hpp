@@ -34,7 +34,7 @@ hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st);
 int wide_panels(int p);
 int64_t wide_stride();
 hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st);
-int wide_gram_wg_per_cu();
+int wide_gram_wg_per_cu(bool diag);
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st);
 hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,
                               int nrow, double* out, hipStream_t st);

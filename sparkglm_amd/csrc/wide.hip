@@ -29,8 +29,11 @@
 #ifndef WIDE_SPREAD_DMA
 #define WIDE_SPREAD_DMA 1
 #endif
-#ifndef WIDE_DIAG2
-#define WIDE_DIAG2 0  // diagonal super-tiles: two blocks per LDS stage / barrier (measured 1 % slower)
+// Workgroups per CU of the diagonal-super-tile kernel.  Its LDS image is one panel per buffer
+// (33.5 KB), so three fit beside each other; measured (tools/ab_wide.sh): three waves per SIMD
+// instead of two change nothing (p = 512 -0.3 %) and spill a few VGPRs, so two.
+#ifndef WIDE_DIAG_WG
+#define WIDE_DIAG_WG 2
 #endif
 
 namespace sglm {
@@ -67,8 +70,11 @@ constexpr int WRB = WIDE_RB;               // rows per block (16)
 constexpr int TB = 16 * WRB + 2;           // doubles per 16-column tile block, padded (258)
 constexpr int PB = PT * TB;                // doubles per panel block image (2064)
 constexpr int OFF_X = 0;                   // [2 buffers][2 panels (I, J)][PB]
-constexpr int OFF_V = 4 * PB;              // [2 buffers][2 slots][w, w*z][WRB]
-constexpr int LDS_DOUBLES = OFF_V + 8 * WRB;
+constexpr int OFF_V = 4 * PB;              // [2 buffers][w, w*z][WRB]
+constexpr int LDS_DOUBLES = OFF_V + 4 * WRB;
+// diagonal-super-tile kernel: [2 buffers][PB] | [2 buffers][w, w*z][WRB]
+constexpr int OFF_VD = 2 * PB;
+constexpr int LDS_DIAG = OFF_VD + 4 * WRB;
 constexpr int NWAVE = 4;                   // one wave per SIMD; two workgroups per CU
 
 __device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
@@ -107,19 +113,17 @@ __device__ __forceinline__ void wstage(double* lds, int buf, const WideGramArgs&
     const int v = wv & 1;  // waves alternate w / w*z (identical redundant copies)
     const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
     if (lane < WRB / 2)
-      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 4 + v) * WRB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + (buf * 2 + v) * WRB), 16, 0, 0);
   }
 }
 
-// Diagonal super-tiles stage TWO blocks per buffer (slot 0 and slot 1 of the panel images the
-// off-diagonal kernel uses for panels I and J), so each barrier covers 2 x 36 MFMAs per wave.
-// This call stages block blk of panel I into slot sl: four octets per wave, and w (waves
-// 2 sl) / w*z (wave 2 sl + 1) of the block.
+// Diagonal super-tiles: stage block blk of panel I into buffer buf of the one-panel image --
+// four octets per wave, and w (wave 0) / w*z (wave 1) of the block.
 template <bool PROC>
-__device__ __forceinline__ void wstage_diag(double* lds, int buf, int sl, const WideGramArgs& a, int64_t blk, int I,
-                                            int wv, const int64_t (&loff)[2], int lane) {
+__device__ __forceinline__ void wstage_diag(double* lds, int buf, const WideGramArgs& a, int64_t blk, int I, int wv,
+                                            const int64_t (&loff)[2], int lane) {
   const double* xb = a.X + blk * WRB;
-  double* dst = lds + OFF_X + (buf * 2 + sl) * PB;
+  double* dst = lds + buf * PB;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int ol = wv * 4 + k;
@@ -136,12 +140,10 @@ __device__ __forceinline__ void wstage_diag(double* lds, int buf, int sl, const 
       }
     }
   }
-  if ((wv >> 1) == sl) {
-    const int v = wv & 1;
-    const double* vsrc = (v ? a.wz : a.w) + blk * WRB + 2 * lane;
+  if (wv < 2) {
+    const double* vsrc = (wv ? a.wz : a.w) + blk * WRB + 2 * lane;
     if (lane < WRB / 2)
-      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_V + ((buf * 2 + sl) * 2 + v) * WRB),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, (lds_void*)(lds + OFF_VD + (buf * 2 + wv) * WRB), 16, 0, 0);
   }
 }
 
@@ -165,7 +167,7 @@ __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv
   const int f = 2 * (cl >> 1);
   const double* xI = lds + OFF_X + (buf * 2 + 0) * PB + cl * WRB + TB * (4 * (wv >> 1));
   const double* xJ = lds + OFF_X + (buf * 2 + 1) * PB + cl * WRB + TB * (4 * (wv & 1));
-  const double* w = lds + OFF_V + (buf * 4 + 0) * WRB;
+  const double* w = lds + OFF_V + (buf * 2 + 0) * WRB;
   double av[2][4], bv[2][4], wr[2];
   auto load = [&](int s, int slot) {
     const int r = 4 * s + rq;
@@ -196,14 +198,14 @@ __device__ __forceinline__ void offdiag_block(const double* lds, int buf, int wv
 // Diagonal super-tile: wave q owns tile rows LO = q and HI = 7-q of the lower tile grid,
 // tiles (LO,0..LO) and (HI,0..HI): 9 tiles, 36 over the four waves; X'Wz on the VALU.
 template <int Q>
-__device__ __forceinline__ void diag_block(const double* lds, int buf, int sl, int lane, d4 (&acc)[9], double& xz_lo,
+__device__ __forceinline__ void diag_block(const double* lds, int buf, int lane, d4 (&acc)[9], double& xz_lo,
                                            double& xz_hi) {
   constexpr int LO = Q, HI = PT - 1 - Q;  // HI >= LO: the B operands are tile columns 0..HI
   const int cl = lane & 15, rq = lane >> 4;
   const int f = 2 * (cl >> 1);
-  const double* xs = lds + OFF_X + (buf * 2 + sl) * PB + cl * WRB;
-  const double* w = lds + OFF_V + ((buf * 2 + sl) * 2 + 0) * WRB;
-  const double* wz = lds + OFF_V + ((buf * 2 + sl) * 2 + 1) * WRB;
+  const double* xs = lds + buf * PB + cl * WRB;
+  const double* w = lds + OFF_VD + (buf * 2 + 0) * WRB;
+  const double* wz = lds + OFF_VD + (buf * 2 + 1) * WRB;
   // operands of k-step s + 1 are read from LDS while the 9 MFMAs of step s issue
   double xv[2][HI + 1], wr[2], wzr[2];
   auto load = [&](int s, int slot) {
@@ -245,31 +247,13 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   int cur = 0;
-  if constexpr (!WIDE_DIAG2) {
-    wstage_diag<PROC>(lds, 0, 0, a, b0, I, wv, loff, lane);
+  wstage_diag<PROC>(lds, 0, a, b0, I, wv, loff, lane);
 #pragma unroll 1
-    for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
-      wait_vm<0>();
-      lds_bar();
-      if (blk + bs < b1) {
-        wstage_diag<PROC>(lds, cur ^ 1, 0, a, blk + bs, I, wv, loff, lane);
-      }
-      diag_block<Q>(lds, cur, 0, lane, acc, xz_lo, xz_hi);
-    }
-  }
-  if constexpr (WIDE_DIAG2) {
-    wstage_diag<PROC>(lds, 0, 0, a, b0, I, wv, loff, lane);
-    if (b0 + bs < b1) wstage_diag<PROC>(lds, 0, 1, a, b0 + bs, I, wv, loff, lane);
-#pragma unroll 1
-    for (int64_t blk = b0; blk < b1; blk += 2 * bs, cur ^= 1) {
-      const int64_t nb = blk + 2 * bs;
-      wait_vm<0>();
-      lds_bar();
-      if (nb < b1) wstage_diag<PROC>(lds, cur ^ 1, 0, a, nb, I, wv, loff, lane);
-      if (nb + bs < b1) wstage_diag<PROC>(lds, cur ^ 1, 1, a, nb + bs, I, wv, loff, lane);
-      diag_block<Q>(lds, cur, 0, lane, acc, xz_lo, xz_hi);
-      if (blk + bs < b1) diag_block<Q>(lds, cur, 1, lane, acc, xz_lo, xz_hi);
-    }
+  for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
+    wait_vm<0>();
+    lds_bar();
+    if (blk + bs < b1) wstage_diag<PROC>(lds, cur ^ 1, a, blk + bs, I, wv, loff, lane);
+    diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
   }
   constexpr int LO = Q, HI = PT - 1 - Q;
 #pragma unroll
@@ -344,8 +328,8 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
 // each gets the whole register file): workgroup g runs the pieces [wg_begin[g],
 // wg_begin[g+1]) of the cost-balanced schedule built on the host (engine.cpp).
 template <bool DIAG, bool PROC>
-__global__ void __launch_bounds__(64 * NWAVE, 2) wide_gram_kernel(WideGramArgs a) {
-  __shared__ double lds[LDS_DOUBLES];
+__global__ void __launch_bounds__(64 * NWAVE, DIAG ? WIDE_DIAG_WG : 2) wide_gram_kernel(WideGramArgs a) {
+  __shared__ double lds[DIAG ? LDS_DIAG : LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pb = a.wg_begin[blockIdx.x], pe = a.wg_begin[blockIdx.x + 1];
@@ -600,7 +584,7 @@ hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-int wide_gram_wg_per_cu() { return 2; }
+int wide_gram_wg_per_cu(bool diag) { return diag ? WIDE_DIAG_WG : 2; }
 
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st) {
   if (diag && a.proc.on)

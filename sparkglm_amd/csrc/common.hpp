@@ -57,6 +57,7 @@ struct PassArgs {
   double* eta_out;      // optional [n]: eta of MODE_IRLS rows (for the final statistics)
   int stats_in_pass;    // narrow binomial/logit IRLS pass without m: pearson / loglik / bad in the
                         // pass's scalars instead of the eta store + stats_kernel
+  int no_gram;          // deviance-only pass (glm_drive's speculative last pass): row stage, no Gram
   int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math,
                         // 32 no eta store
 };

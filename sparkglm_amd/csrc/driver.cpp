@@ -112,7 +112,7 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
   if (rc) return rc;
   double dev = fac * packed[tri_count(p) + p + S_DEV];
   const double null_dev = dev;  // GLM.scala:272 / 444
-  double deltad = 1.0;
+  double deltad = 1.0, d_prev = 0.0;  // d_prev: |deltad| of the iteration before (speculation)
   int iter = 0;
   if (out->dev_trace && out->max_trace > 0) out->dev_trace[0] = dev;
 
@@ -125,9 +125,28 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
       if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
       return srv;
     }
-    rc = be.pass(MODE_IRLS, beta.data(), ymean, 0.0, o.family, o.link, packed.data());
-    if (rc) return rc;
+    // Speculative last pass: IRLS converges quadratically, so from the last two changes the next
+    // one is predicted as d_k^3 / d_{k-1}^2; when that is below tol / 10 the pass at beta is run
+    // without its Gram (which only the next solve would use).  If the deviance then shows no
+    // convergence after all, the full pass at the same beta follows -- the scalars are bitwise
+    // those of the full pass either way, so the fit is identical with or without speculation.
+    bool spec = false;
+    if (be.has_dev_pass() && iter >= 2 && d_prev > 0.0 && !(o.max_iter > 0 && iter + 1 >= o.max_iter)) {
+      const double dk = std::fabs(deltad);
+      spec = dk * dk * dk < 0.1 * o.tol * d_prev * d_prev;
+    }
+    if (spec) {
+      rc = be.pass_dev(MODE_IRLS, beta.data(), ymean, 0.0, o.family, o.link, packed.data());
+      if (rc) return rc;
+      if (!(std::fabs(fac * packed[tri_count(p) + p + S_DEV] - dev) <= o.tol))
+        spec = false;  // not the last iteration after all: the full pass at the same beta
+    }
+    if (!spec) {
+      rc = be.pass(MODE_IRLS, beta.data(), ymean, 0.0, o.family, o.link, packed.data());
+      if (rc) return rc;
+    }
     const double dev_old = dev;
+    d_prev = std::fabs(deltad);
     dev = fac * packed[tri_count(p) + p + S_DEV];
     deltad = dev - dev_old;
     iter = iter + 1;

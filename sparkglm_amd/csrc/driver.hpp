@@ -58,6 +58,12 @@ class Backend {
   // True when the last MODE_IRLS pass also delivered the final statistics (pearson, loglik
   // ingredients, bad) in its packed scalars, so glm_drive needs no stats() pass.
   virtual bool pass_has_stats() const { return false; }
+  // Deviance-only pass: the scalars of pass() at beta (bitwise), no Gram.  glm_drive runs it
+  // for an iteration it predicts to be the last (the Gram of that pass would go unused).
+  virtual bool has_dev_pass() const { return false; }
+  virtual int pass_dev(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) {
+    return pass(mode, beta, mu0, ybar, family, link, packed);
+  }
   // The solver for this backend's systems (default: host).
   virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats

@@ -121,6 +121,9 @@ struct sglm_engine : public Backend {
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
   bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
+  // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
+  // scalar reduction but no Gram -- bitwise the scalars of the full pass.  SGLM_SPECULATE=0 off.
+  bool dev_only = false, allow_spec = true;
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
   // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; SGLM_NARROW=0 disables
@@ -146,7 +149,7 @@ struct sglm_engine : public Backend {
   hipEvent_t evm = nullptr;
   rocblas_handle blas = nullptr;
   // stats
-  int64_t passes = 0;
+  int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
@@ -709,6 +712,17 @@ struct sglm_engine : public Backend {
     return allreduce_small(out2, 2);
   }
 
+  bool has_dev_pass() const override { return allow_spec; }
+  int pass_dev(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
+    for (sglm_engine* s : subs) s->dev_only = true;
+    dev_only = true;
+    const int rc = pass(mode, beta, mu0, ybar, family, link, packed);
+    for (sglm_engine* s : subs) s->dev_only = false;
+    dev_only = false;
+    dev_passes += 1;
+    return rc;
+  }
+
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
     if (group()) return group_pass(mode, beta, mu0, ybar, family, link, packed);
     int rc = enqueue_pass(mode, beta, mu0, ybar, family, link);
@@ -790,6 +804,7 @@ struct sglm_engine : public Backend {
                        !force_eta_store) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
     a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
+    a.no_gram = dev_only ? 1 : 0;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (wide) {
@@ -831,7 +846,7 @@ struct sglm_engine : public Backend {
         g.X = dxsc;
         g.ld = ch_rows;
         g.proc = ProcX{};
-        r.xs_out = dxsc;
+        r.xs_out = dev_only ? nullptr : dxsc;  // deviance only: eta from the generator, no scratch
         r.xs_ld = ch_rows;
         for (int c = 0; c < nch; ++c) {
           r.r_begin = (int64_t)c * ch_rows;
@@ -841,7 +856,7 @@ struct sglm_engine : public Backend {
           HIPCHK(hipEventRecord(evch[(size_t)2 * c + 1], st));
           g.w = dw + r.r_begin;
           g.wz = dwz + r.r_begin;
-          for (int kind = 0; kind < 2; ++kind) {
+          for (int kind = 0; kind < 2 && !dev_only; ++kind) {
             if (!has_sched[kind]) continue;
             g.pieces = dpieces[kind];
             g.wg_begin = dwgb[kind];
@@ -857,7 +872,7 @@ struct sglm_engine : public Backend {
       }
       HIPCHK(launch_wide_rows(r, rgrid, st));
       HIPCHK(hipEventRecord(evm, st));
-      for (int kind = 0; kind < 2; ++kind) {
+      for (int kind = 0; kind < 2 && !dev_only; ++kind) {
         if (!has_sched[kind]) continue;
         g.pieces = dpieces[kind];
         g.wg_begin = dwgb[kind];
@@ -1230,6 +1245,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
+  if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
   *out = h;
   return SGLM_OK;
 }

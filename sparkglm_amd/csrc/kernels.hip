@@ -314,7 +314,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
-  const bool do_gram = !(SGLM_DBG(a) & 2);
+  const bool do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram;
   // roles are compile-time per wave (WV), so each wave's instantiation carries only its code
   constexpr int rw = WV - G::ROW0;
   constexpr bool row_wave = rw >= 0 && rw < G::NRW;

@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   const int cl1 = (cl + 4) & 15, cl2 = (cl + 8) & 15;
   const int off1 = cl1 * NRB - cl * NRB, off2 = cl2 * NRB - cl * NRB;
   const int fc1 = swz<NRB>(cl1), fc2 = swz<NRB>(cl2);
-  const bool do_rows = !(SGLM_DBG(a) & 1), do_gram = !(SGLM_DBG(a) & 2), do_dma = !(SGLM_DBG(a) & 4);
+  const bool do_rows = !(SGLM_DBG(a) & 1), do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram, do_dma = !(SGLM_DBG(a) & 4);
 
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
   if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);

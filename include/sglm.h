@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 2
+#define SGLM_ABI_VERSION 3  /* 3: sglm_stats.dev_passes */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -141,6 +141,9 @@ typedef struct {
   int64_t load_bytes;       /* bytes those calls moved to the device */
   int ndev;                 /* devices driven by this handle */
   int rccl_group;           /* multi-device handle reducing over RCCL (1) or on the host (0) */
+  int64_t dev_passes;       /* deviance-only passes: iterations the fit predicted to be its last
+                               (quadratic convergence) ran without the unused Gram; bitwise the
+                               scalars of the full pass (SGLM_SPECULATE=0 disables) */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device

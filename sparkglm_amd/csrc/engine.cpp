@@ -1269,6 +1269,7 @@ int sglm_create_multi(const int* devs, int ndev, sglm_engine** out) {
     }
     g->subs.push_back(s);
   }
+  g->allow_spec = g->subs[0]->allow_spec;  // the group handle drives the fit (SGLM_SPECULATE)
   bool distinct = true;
   for (int a = 0; a < ndev; ++a)
     for (int b = 0; b < a; ++b) distinct = distinct && devs[a] != devs[b];
@@ -1669,6 +1670,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
     out->solve_ms = h->solve_ms;
     out->ndev = (int)h->subs.size();
     out->rccl_group = h->gcomms.empty() ? 0 : 1;
+    out->dev_passes = h->dev_passes;
     return SGLM_OK;
   }
   out->passes = h->passes;
@@ -1689,13 +1691,14 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->load_bytes = h->load_bytes;
   out->ndev = 1;
   out->rccl_group = 0;
+  out->dev_passes = h->dev_passes;
   return SGLM_OK;
 }
 
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
-  h->passes = 0;
+  h->passes = h->dev_passes = 0;
   h->pass_ms = h->reduce_ms = h->last_pass_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;

@@ -35,6 +35,9 @@
 #ifndef WIDE_DIAG_WG
 #define WIDE_DIAG_WG 2
 #endif
+#ifndef WIDE_DIAG_BATCH
+#define WIDE_DIAG_BATCH 0  // diagonal k-steps: operands and VALU of the whole block before its MFMAs
+#endif
 
 namespace sglm {
 
@@ -206,6 +209,30 @@ __device__ __forceinline__ void diag_block(const double* lds, int buf, int lane,
   const double* xs = lds + buf * PB + cl * WRB;
   const double* w = lds + OFF_VD + (buf * 2 + 0) * WRB;
   const double* wz = lds + OFF_VD + (buf * 2 + 1) * WRB;
+#if WIDE_DIAG_BATCH
+  // every operand of the block's 4 k-steps first, the VALU scaling, then 36 MFMAs back to back
+  double xb[WRB / 4][HI + 1], al[WRB / 4], ah[WRB / 4];
+#pragma unroll
+  for (int s = 0; s < WRB / 4; ++s) {
+    const int r = 4 * s + rq;
+    const int o = r ^ f;
+    const double wr = w[r], wzr = wz[r];
+#pragma unroll
+    for (int c = 0; c <= HI; ++c) xb[s][c] = xs[o + TB * c];
+    al[s] = xb[s][LO] * wr;
+    ah[s] = xb[s][HI] * wr;
+    xz_lo += xb[s][LO] * wzr;
+    xz_hi += xb[s][HI] * wzr;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < WRB / 4; ++s)
+#pragma unroll
+    for (int k = 0; k <= PT; ++k)
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? al[s] : ah[s], xb[s][k <= LO ? k : k - LO - 1], acc[k], 0,
+                                                    0, 0);
+  return;
+#endif
   // operands of k-step s + 1 are read from LDS while the 9 MFMAs of step s issue
   double xv[2][HI + 1], wr[2], wzr[2];
   auto load = [&](int s, int slot) {

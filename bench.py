@@ -255,7 +255,7 @@ def main() -> int:
         if wide:
             kern = "wide_gram_kernel"
             kern_ms = st["gram_kernel_ms"] / passes
-            pass_ms = (st["gram_kernel_ms"] + st["row_kernel_ms"]) / passes
+            pass_ms = st["pass_kernel_ms"] / passes  # wall span of the pass (row and Gram may overlap)
         elif st["path"] == 2:
             kern = f"irls_narrow_kernel<{(p + 15) // 16},{fam},{lnk}>"
             kern_ms = st["pass_kernel_ms"] / passes

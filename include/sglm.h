@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 3  /* 3: sglm_stats.dev_passes */
+#define SGLM_ABI_VERSION 4  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -144,6 +144,9 @@ typedef struct {
   int64_t dev_passes;       /* deviance-only passes: iterations the fit predicted to be its last
                                (quadratic convergence) ran without the unused Gram; bitwise the
                                scalars of the full pass (SGLM_SPECULATE=0 disables) */
+  int overlap_chunks;       /* wide path, resident X: chunks per pass whose row kernel runs on a
+                               second stream beside the previous chunk's Gram (0: not overlapped;
+                               SGLM_WIDE_OVERLAP sets the count, SGLM_WIDE_OV_MIN the fewest rows) */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device

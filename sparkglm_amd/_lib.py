@@ -60,7 +60,8 @@ class Stats(C.Structure):
                 ("n_local", C.c_int64), ("p", C.c_int64), ("workgroups", C.c_int), ("kernel_variant", C.c_int),
                 ("path", C.c_int), ("wide_panels", C.c_int), ("row_kernel_ms", C.c_double),
                 ("gram_kernel_ms", C.c_double), ("load_ms", C.c_double), ("load_bytes", C.c_int64),
-                ("ndev", C.c_int), ("rccl_group", C.c_int), ("dev_passes", C.c_int64)]
+                ("ndev", C.c_int), ("rccl_group", C.c_int), ("dev_passes", C.c_int64),
+                ("overlap_chunks", C.c_int)]
 
 
 class GlmDerived(C.Structure):

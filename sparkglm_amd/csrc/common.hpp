@@ -121,6 +121,7 @@ struct WideGramArgs {
   int64_t stride;
   int dbg;              // profiling ablations: 4 DMA, 32 barriers
   ProcX proc;
+  int64_t nb_lim;       // blocks of this launch's rows: pieces are clipped to [b0, min(b1, nb_lim))
 };
 
 // Arguments of the final-statistics pass (stats_kernel).

@@ -138,6 +138,17 @@ struct sglm_engine : public Backend {
   std::vector<hipEvent_t> evch;  // [2 * nch]: row-kernel span of each chunk
   double *dxsc = nullptr, *dchunks = nullptr;
   bool allow_chunks = true;  // SGLM_PROC_CHUNKS=0 disables
+  // resident wide shards, overlapped passes: the rows are cut into nov chunks; the row kernel of
+  // chunk c + 1 runs on a second stream (st2) beside the Gram kernels of chunk c, so only chunk 0's
+  // row stage is exposed.  Each chunk is reduced into dchunks[c]; the chunks are summed in order.
+  int ov_want = 16;                // SGLM_WIDE_OVERLAP: chunks per pass (<= 1: off)
+  int64_t ov_min = (int64_t)1 << 16;  // SGLM_WIDE_OV_MIN: fewest rows per chunk (fewer chunks on small shards)
+  int nov = 0;
+  int64_t ov_rows = 0;             // rows per chunk (multiple of 32; the last chunk may be shorter)
+  int rgrid_ov = 0;                // row-kernel grid of chunks >= 1 (one workgroup per CU)
+  bool ov_serial = false;          // SGLM_WIDE_OV_SERIAL=1: the chunks' row kernels on st (A/B only)
+  hipStream_t st2 = nullptr;
+  std::vector<hipEvent_t> evov;    // [4 * nov + 1]: row span, Gram span per chunk; st -> st2 fork
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
   int64_t gp_cap = 0, rp_cap = 0, wstride = 0;
   int npan = 0, nst = 0, nslots = 0, ggrid = 0, rgrid = 0;
@@ -193,6 +204,8 @@ struct sglm_engine : public Backend {
     }
     ch_rows = 0;
     nch = 0;
+    nov = 0;
+    ov_rows = 0;
   }
   void release() {
     (void)hipSetDevice(device);
@@ -222,6 +235,10 @@ struct sglm_engine : public Backend {
     comm.nccl = nullptr;
     for (hipEvent_t e : evch) (void)hipEventDestroy(e);
     evch.clear();
+    for (hipEvent_t e : evov) (void)hipEventDestroy(e);
+    evov.clear();
+    if (st2) (void)hipStreamDestroy(st2);
+    st2 = nullptr;
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
@@ -309,7 +326,7 @@ struct sglm_engine : public Backend {
   int wide_band = 1;  // SGLM_WIDE_BAND: 0 contiguous cost-balanced pieces, 1 banded
   bool banded_kind(int S, int64_t nb, int G) const { return wide_band != 0 && S > 0 && G / S >= 2 && nb >= 2; }
   int build_wide_schedule() {
-    const int64_t nb = (nch > 0 ? ch_rows : n_pad) / WIDE_RB;
+    const int64_t nb = (nch > 0 ? ch_rows : nov > 0 ? ov_rows : n_pad) / WIDE_RB;
     std::vector<int> str((size_t)nst * 2, 0);
     free_schedule();
     int slot = 0;
@@ -406,10 +423,29 @@ struct sglm_engine : public Backend {
     ggk[0] = ncu * wide_gram_wg_per_cu(false);
     ggk[1] = ncu * wide_gram_wg_per_cu(true);
     ggrid = ggk[0];
+    nov = 0;
+    ov_rows = 0;
+    if (!procx.on && dX && ov_want > 1 && n_pad >= 2 * ov_min) {
+      ov_rows = (std::max<int64_t>(ov_min, (n_pad + ov_want - 1) / ov_want) + 31) / 32 * 32;
+      nov = (int)((n_pad + ov_rows - 1) / ov_rows);
+      if (nov < 2) nov = 0, ov_rows = 0;
+    }
+    if (nov > 1) {
+      if (!st2) HIPCHK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+      while (evov.size() < (size_t)4 * nov + 1) {
+        hipEvent_t e = nullptr;
+        HIPCHK(hipEventCreate(&e));
+        evov.push_back(e);
+      }
+      if (dchunks) HIPCHK(hipFree(dchunks));
+      dchunks = nullptr;
+      HIPCHK(hipMalloc(&dchunks, sizeof(double) * (size_t)nov * (size_t)packed_len(p)));
+    }
     int rc = build_wide_schedule();
     if (rc) return rc;
     grid = nslots;
-    rgrid = (int)std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ncu, (n_pad + 255) / 256));
+    rgrid = (int)std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ncu, ((nov > 0 ? ov_rows : n_pad) + 255) / 256));
+    rgrid_ov = std::min(rgrid, ncu);
     const int64_t need_gp = (int64_t)std::max(nslots, 1) * wstride;
     if (need_gp > gp_cap) {
       if (dgp) HIPCHK(hipFree(dgp));
@@ -417,7 +453,9 @@ struct sglm_engine : public Backend {
       HIPCHK(hipMalloc(&dgp, sizeof(double) * need_gp));
       gp_cap = need_gp;
     }
-    const int64_t need_rp = (int64_t)rgrid * NS;
+    // overlapped passes keep every chunk's row partials until its reduce (the next chunk's row
+    // kernel runs meanwhile): chunk 0 at [0, rgrid), chunk c >= 1 at rgrid + (c - 1) rgrid_ov
+    const int64_t need_rp = ((int64_t)rgrid + (nov > 1 ? (int64_t)(nov - 1) * rgrid_ov : 0)) * NS;
     if (need_rp > rp_cap) {
       if (drp) HIPCHK(hipFree(drp));
       drp = nullptr;
@@ -752,7 +790,18 @@ struct sglm_engine : public Backend {
     HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
     if (wide) {
       float km = 0.f;
-      if (nch > 0) {  // chunked procedural pass: the row kernels' spans, the rest is Gram
+      if (nov > 0) {  // overlapped pass: row spans (st2) and Gram spans (st) summed separately
+        float kg = 0.f;
+        for (int c = 0; c < nov; ++c) {
+          float kr = 0.f, kc = 0.f;
+          HIPCHK(hipEventElapsedTime(&kr, evov[(size_t)4 * c], evov[(size_t)4 * c + 1]));
+          HIPCHK(hipEventElapsedTime(&kc, evov[(size_t)4 * c + 2], evov[(size_t)4 * c + 3]));
+          km += kr;
+          kg += kc;
+        }
+        row_ms += km;
+        gram_ms += kg;
+      } else if (nch > 0) {  // chunked procedural pass: the row kernels' spans, the rest is Gram
         for (int c = 0; c < nch; ++c) {
           float kc = 0.f;
           HIPCHK(hipEventElapsedTime(&kc, evch[(size_t)2 * c], evch[(size_t)2 * c + 1]));
@@ -761,8 +810,10 @@ struct sglm_engine : public Backend {
       } else {
         HIPCHK(hipEventElapsedTime(&km, ev0, evm));
       }
-      row_ms += km;
-      gram_ms += k1 - km;
+      if (nov == 0) {
+        row_ms += km;
+        gram_ms += k1 - km;
+      }
     }
     passes += 1;
     pass_ms += k1;
@@ -841,6 +892,7 @@ struct sglm_engine : public Backend {
       g.stride = wstride;
       g.dbg = dbg;
       g.proc = procx;
+      g.nb_lim = INT64_MAX;
       if (nch > 0) {  // procedural shard in chunks: generate C rows into the scratch, resident Gram over it
         const int64_t plen = packed_len(p);
         g.X = dxsc;
@@ -867,6 +919,46 @@ struct sglm_engine : public Backend {
         HIPCHK(hipEventRecord(evm, st));  // unused in chunked timing (pass_timing sums evch)
         HIPCHK(hipEventRecord(ev1, st));
         HIPCHK(launch_sum_chunks(dchunks, nch, (int)p, dred, st));
+        HIPCHK(hipEventRecord(ev2, st));
+        return SGLM_OK;
+      }
+      if (nov > 0) {  // overlapped chunks: row kernels on st2, chunk c's Gram on st once its rows are done
+        const int64_t plen = packed_len(p);
+        auto rows_of = [&](int c, int64_t& r0, int64_t& r1) {
+          r0 = (int64_t)c * ov_rows;
+          r1 = std::min<int64_t>(n_pad, r0 + ov_rows);
+        };
+        auto rowpart = [&](int c) { return drp + (c == 0 ? 0 : ((int64_t)rgrid + (int64_t)(c - 1) * rgrid_ov) * NS); };
+        HIPCHK(hipEventRecord(evov[(size_t)4 * nov], st));  // fork: beta uploaded, the last pass's Gram done
+        HIPCHK(hipStreamWaitEvent(st2, evov[(size_t)4 * nov], 0));
+        for (int c = 0; c < nov; ++c) {
+          rows_of(c, r.r_begin, r.r_end);
+          r.row_partials = rowpart(c);
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c], ov_serial ? st : st2));
+          HIPCHK(launch_wide_rows(r, c == 0 ? rgrid : rgrid_ov, ov_serial ? st : st2, c > 0));
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c + 1], ov_serial ? st : st2));
+        }
+        for (int c = 0; c < nov; ++c) {
+          int64_t r0 = 0, r1 = 0;
+          rows_of(c, r0, r1);
+          HIPCHK(hipStreamWaitEvent(st, evov[(size_t)4 * c + 1], 0));
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c + 2], st));
+          g.X = dX + r0;
+          g.w = dw + r0;
+          g.wz = dwz + r0;
+          g.nb_lim = (r1 - r0) / WIDE_RB;
+          for (int kind = 0; kind < 2 && !dev_only; ++kind) {
+            if (!has_sched[kind]) continue;
+            g.pieces = dpieces[kind];
+            g.wg_begin = dwgb[kind];
+            HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+          }
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c + 3], st));
+          HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, rowpart(c), c == 0 ? rgrid : rgrid_ov,
+                                    dchunks + (int64_t)c * plen, st));
+        }
+        HIPCHK(hipEventRecord(ev1, st));
+        HIPCHK(launch_sum_chunks(dchunks, nov, (int)p, dred, st));
         HIPCHK(hipEventRecord(ev2, st));
         return SGLM_OK;
       }
@@ -1245,6 +1337,9 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
+  if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
+  if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
+  if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
   *out = h;
   return SGLM_OK;
@@ -1671,6 +1766,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
     out->ndev = (int)h->subs.size();
     out->rccl_group = h->gcomms.empty() ? 0 : 1;
     out->dev_passes = h->dev_passes;
+    out->overlap_chunks = h->subs.empty() ? 0 : h->subs[0]->nov;
     return SGLM_OK;
   }
   out->passes = h->passes;
@@ -1692,6 +1788,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->ndev = 1;
   out->rccl_group = 0;
   out->dev_passes = h->dev_passes;
+  out->overlap_chunks = h->nov;
   return SGLM_OK;
 }
 

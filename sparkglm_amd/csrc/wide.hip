@@ -42,6 +42,7 @@
 namespace sglm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 namespace {
@@ -274,7 +275,7 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   int cur = 0;
-  wstage_diag<PROC>(lds, 0, a, b0, I, wv, loff, lane);
+  if (b0 < b1) wstage_diag<PROC>(lds, 0, a, b0, I, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
     wait_vm<0>();
@@ -309,7 +310,7 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   const int dbg = SGLM_DBG(a);
   int64_t loff[2];
   lane_offsets(a, lane, loff);
-  wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
+  if (b0 < b1) wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
   int cur = 0;
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
@@ -363,19 +364,20 @@ __global__ void __launch_bounds__(64 * NWAVE, DIAG ? WIDE_DIAG_WG : 2) wide_gram
 #pragma unroll 1
   for (int pc = pb; pc < pe; ++pc) {
     const WidePiece pz = a.pieces[pc];
+    const int64_t b1 = pz.b1 < a.nb_lim ? pz.b1 : a.nb_lim;  // a shorter last chunk clips the schedule
     const int st = pz.st;
     int I = 0;
     while ((I + 1) * (I + 2) / 2 <= st) ++I;
     const int J = st - I * (I + 1) / 2;
     double* out = a.partials + (int64_t)pz.slot * a.stride;
     if constexpr (!DIAG) {
-      offdiag_piece<PROC>(lds, a, I, J, pz.b0, pz.b1, pz.bs, wv, lane, out);
+      offdiag_piece<PROC>(lds, a, I, J, pz.b0, b1, pz.bs, wv, lane, out);
     } else {
       switch (wv) {
-        case 0: diag_piece<0, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
-        case 1: diag_piece<1, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
-        case 2: diag_piece<2, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
-        default: diag_piece<3, PROC>(lds, a, I, pz.b0, pz.b1, pz.bs, wv, lane, out); break;
+        case 0: diag_piece<0, PROC>(lds, a, I, pz.b0, b1, pz.bs, wv, lane, out); break;
+        case 1: diag_piece<1, PROC>(lds, a, I, pz.b0, b1, pz.bs, wv, lane, out); break;
+        case 2: diag_piece<2, PROC>(lds, a, I, pz.b0, b1, pz.bs, wv, lane, out); break;
+        default: diag_piece<3, PROC>(lds, a, I, pz.b0, b1, pz.bs, wv, lane, out); break;
       }
     }
     lds_bar();  // every wave is done with both buffers before the next piece stages
@@ -385,12 +387,9 @@ __global__ void __launch_bounds__(64 * NWAVE, DIAG ? WIDE_DIAG_WG : 2) wide_gram
 // Row stage: thread per row QUAD (two 16-byte loads of four adjacent rows of each column: a
 // wave reads 2 KiB contiguous per column), columns streamed in order with four partial sums
 // per row (the per-row summation order does not depend on the rows per thread).
-template <int FAM, int LNK>
-__global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
-#ifndef SGLM_WIDE_RPT
-#define SGLM_WIDE_RPT 4
-#endif
-  constexpr int RPT = SGLM_WIDE_RPT;  // rows per thread (even, divides 32)
+template <int FAM, int LNK, int RPT, bool NT = false>
+__device__ __forceinline__ void wide_rows_body(const WideRowArgs& a) {
+  static_assert(RPT % 2 == 0 && 32 % RPT == 0, "rows per thread: even, divides 32");
   __shared__ double red[4][2];
   const int64_t q0 = a.r_begin / RPT, nq = (a.r_end - a.r_begin) / RPT;  // row quads of this launch
   const int64_t per = (nq + gridDim.x - 1) / gridDim.x;
@@ -451,7 +450,14 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
             const double b = a.beta[j + q];
 #pragma unroll
             for (int h = 0; h < RPT / 2; ++h) {
-              const double2 v = *(const double2*)(xc + (int64_t)(j + q) * a.ld + 2 * h);
+              const double2* src = (const double2*)(xc + (int64_t)(j + q) * a.ld + 2 * h);
+              double2 v;
+              if constexpr (NT) {
+                const dv2 t = __builtin_nontemporal_load((const dv2*)src);
+                v = double2{t.x, t.y};
+              } else {
+                v = *src;
+              }
               e[2 * h][q] += v.x * b;
               e[2 * h + 1][q] += v.y * b;
             }
@@ -507,6 +513,26 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
     if (k == S_SUMW) v = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
     a.row_partials[(int64_t)blockIdx.x * NS + k] = v;
   }
+}
+
+#ifndef SGLM_WIDE_RPT
+#define SGLM_WIDE_RPT 4
+#endif
+#ifndef WIDE_ROW_NT
+#define WIDE_ROW_NT 1  // overlapped row kernel: non-temporal X loads (keep the Gram's rows in the caches)
+#endif
+template <int FAM, int LNK>
+__global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
+  wide_rows_body<FAM, LNK, SGLM_WIDE_RPT>(a);
+}
+
+// The same row stage for the overlapped chunks (engine.cpp enqueue_pass): one workgroup per CU
+// beside the two persistent Gram workgroups, so at most 96 VGPRs (2 x 208 + 96 = the SIMD's
+// 512) and two rows per thread (no spills at that budget).  Per-row arithmetic and order are the
+// full kernel's, bit for bit.
+template <int FAM, int LNK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) wide_rows_ov_kernel(WideRowArgs a) {
+  wide_rows_body<FAM, LNK, 2, WIDE_ROW_NT != 0>(a);
 }
 
 // Packed output: lower-tri X'WX row-major | X'Wz | NS scalars, summed in a fixed order.
@@ -590,25 +616,42 @@ __global__ void unpack_lower_kernel(const double* __restrict__ packed, int p, do
 int wide_panels(int p) { return (p + PANEL - 1) / PANEL; }
 int64_t wide_stride() { return (int64_t)PT * PT * 256 + PANEL; }
 
-hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st) {
-  const dim3 g(grid), b(256);
-  const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
-  const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+#define SGLM_ROW_LAUNCH(KN)                                                                    \
+  template <int F, int L>                                                                      \
+  struct KN##_t {                                                                              \
+    static void go(dim3 g, dim3 b, hipStream_t st, const WideRowArgs& a) {                     \
+      hipLaunchKernelGGL((KN<F, L>), g, b, 0, st, a);                                          \
+    }                                                                                          \
+  };
+SGLM_ROW_LAUNCH(wide_rows_kernel)
+SGLM_ROW_LAUNCH(wide_rows_ov_kernel)
+#undef SGLM_ROW_LAUNCH
+
+template <template <int, int> class K>
+static hipError_t launch_rows_fl(int fam, int lnk, dim3 g, dim3 b, hipStream_t st, const WideRowArgs& a) {
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
+    K<FAM_BINOMIAL, LNK_LOGIT>::go(g, b, st, a);
   else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, a);
+    K<FAM_BINOMIAL, LNK_PROBIT>::go(g, b, st, a);
   else if (fam == FAM_BINOMIAL)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, a);
+    K<FAM_BINOMIAL, LNK_CLOGLOG>::go(g, b, st, a);
   else if (fam == FAM_GAUSSIAN)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, a);
+    K<FAM_GAUSSIAN, LNK_IDENTITY>::go(g, b, st, a);
   else if (fam == FAM_POISSON)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_POISSON, LNK_LOG>), g, b, 0, st, a);
+    K<FAM_POISSON, LNK_LOG>::go(g, b, st, a);
   else if (fam == FAM_GAMMA)
-    hipLaunchKernelGGL((wide_rows_kernel<FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, a);
+    K<FAM_GAMMA, LNK_INVERSE>::go(g, b, st, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st, bool ov) {
+  const dim3 g(grid), b(256);
+  const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
+  const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  return ov ? launch_rows_fl<wide_rows_ov_kernel_t>(fam, lnk, g, b, st, a)
+            : launch_rows_fl<wide_rows_kernel_t>(fam, lnk, g, b, st, a);
 }
 
 int wide_gram_wg_per_cu(bool diag) { return diag ? WIDE_DIAG_WG : 2; }

@@ -135,9 +135,16 @@ struct sglm_engine : public Backend {
   // over it -- X is generated once per pass instead of once per super-tile that reads it
   int64_t ch_rows = 0;  // rows per chunk (multiple of 32); 0: in-kernel generation (PROC kernels)
   int nch = 0;
-  std::vector<hipEvent_t> evch;  // [2 * nch]: row-kernel span of each chunk
+  std::vector<hipEvent_t> evch;  // [4 * nch + 1]: row span, Gram span per chunk; st -> st2 fork
   double *dxsc = nullptr, *dchunks = nullptr;
   bool allow_chunks = true;  // SGLM_PROC_CHUNKS=0 disables
+  // SGLM_PROC_OVERLAP: chunks of an overlapped procedural pass (<= 1: one buffer, serial).  Off:
+  // measured (250M x 512 logit) 1257 ms per pass serial, 1420 / 1480 ms at 8 / 16 chunks -- the
+  // generating row kernel's integer + fp64 VALU shares the SIMDs with the Gram's MFMAs and slows
+  // them by 31-38 %, more than the 193 ms of row kernels it hides.
+  int proc_ov_want = 0;
+  bool proc_ov = false;      // double-buffered scratch, row kernels on st2 (as the resident overlap below)
+  int64_t proc_ov_min = (int64_t)1 << 20;  // SGLM_PROC_OV_MIN: fewest rows per overlapped chunk
   // resident wide shards, overlapped passes: the rows are cut into nov chunks; the row kernel of
   // chunk c + 1 runs on a second stream (st2) beside the Gram kernels of chunk c, so only chunk 0's
   // row stage is exposed.  Each chunk is reduced into dchunks[c]; the chunks are summed in order.
@@ -204,6 +211,7 @@ struct sglm_engine : public Backend {
     }
     ch_rows = 0;
     nch = 0;
+    proc_ov = false;
     nov = 0;
     ov_rows = 0;
   }
@@ -416,6 +424,10 @@ struct sglm_engine : public Backend {
     return SGLM_OK;
   }
 
+  // chunks whose row kernels run beside the Gram (resident or procedural), 0 if none
+  int ov_chunks() const { return nov > 1 ? nov : (proc_ov ? nch : 0); }
+  double* rowpart(int c) const { return drp + (c == 0 ? 0 : ((int64_t)rgrid + (int64_t)(c - 1) * rgrid_ov) * NS); }
+
   int ensure_wide_workspace() {
     npan = wide_panels((int)p);
     nst = npan * (npan + 1) / 2;
@@ -455,7 +467,7 @@ struct sglm_engine : public Backend {
     }
     // overlapped passes keep every chunk's row partials until its reduce (the next chunk's row
     // kernel runs meanwhile): chunk 0 at [0, rgrid), chunk c >= 1 at rgrid + (c - 1) rgrid_ov
-    const int64_t need_rp = ((int64_t)rgrid + (nov > 1 ? (int64_t)(nov - 1) * rgrid_ov : 0)) * NS;
+    const int64_t need_rp = ((int64_t)rgrid + (int64_t)(std::max(ov_chunks(), 1) - 1) * rgrid_ov) * NS;
     if (need_rp > rp_cap) {
       if (drp) HIPCHK(hipFree(drp));
       drp = nullptr;
@@ -477,12 +489,22 @@ struct sglm_engine : public Backend {
     const int64_t cap_rows = fr > margin ? (int64_t)((fr - margin) / (sizeof(double) * (size_t)ncols8)) : 0;
     int64_t c = std::min<int64_t>(n_pad, cap_rows / 32 * 32);
     if (c < std::min<int64_t>(n_pad, (int64_t)1 << 20)) return SGLM_OK;  // too little room: in-kernel generation
-    const int64_t k = (n_pad + c - 1) / c;
+    int64_t k = (n_pad + c - 1) / c;
+    // overlapped: two scratch buffers, the row kernel of chunk c + 1 generates into one while the
+    // Gram kernels of chunk c read the other; at least proc_ov_want chunks of >= 1M rows
+    const int64_t half = cap_rows / 2 / 32 * 32, kmin = proc_ov_min;
+    proc_ov = false;
+    if (proc_ov_want > 1 && half >= kmin && n_pad >= 2 * kmin) {
+      k = std::max<int64_t>((n_pad + half - 1) / half, std::min<int64_t>(proc_ov_want, n_pad / kmin));
+      proc_ov = k >= 2;
+    }
     c = ((n_pad + k - 1) / k + 31) / 32 * 32;
     ch_rows = c;
     nch = (int)((n_pad + c - 1) / c);
-    HIPCHK(hipMalloc(&dxsc, sizeof(double) * (size_t)c * (size_t)ncols8));
-    HIPCHK(hipMemsetAsync(dxsc, 0, sizeof(double) * (size_t)c * (size_t)ncols8, st));
+    const size_t sc = sizeof(double) * (size_t)c * (size_t)ncols8 * (proc_ov ? 2 : 1);
+    HIPCHK(hipMalloc(&dxsc, sc));
+    HIPCHK(hipMemsetAsync(dxsc, 0, sc, st));
+    if (proc_ov && !st2) HIPCHK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
     const int64_t span = (int64_t)nch * c;  // w / w*z rows the chunks address
     if (span > n_pad) {
       for (double** q : {&dw, &dwz}) {
@@ -493,7 +515,7 @@ struct sglm_engine : public Backend {
       }
     }
     HIPCHK(hipMalloc(&dchunks, sizeof(double) * (size_t)nch * (size_t)packed_len(p)));
-    while (evch.size() < (size_t)2 * nch) {
+    while (evch.size() < (size_t)4 * nch + 1) {
       hipEvent_t e = nullptr;
       HIPCHK(hipEventCreate(&e));
       evch.push_back(e);
@@ -790,27 +812,20 @@ struct sglm_engine : public Backend {
     HIPCHK(hipEventElapsedTime(&k2, ev1, ev2));
     if (wide) {
       float km = 0.f;
-      if (nov > 0) {  // overlapped pass: row spans (st2) and Gram spans (st) summed separately
+      if (nov > 0 || nch > 0) {  // chunked pass: row spans and Gram spans per chunk
+        const std::vector<hipEvent_t>& ev = nov > 0 ? evov : evch;
         float kg = 0.f;
-        for (int c = 0; c < nov; ++c) {
+        for (int c = 0; c < (nov > 0 ? nov : nch); ++c) {
           float kr = 0.f, kc = 0.f;
-          HIPCHK(hipEventElapsedTime(&kr, evov[(size_t)4 * c], evov[(size_t)4 * c + 1]));
-          HIPCHK(hipEventElapsedTime(&kc, evov[(size_t)4 * c + 2], evov[(size_t)4 * c + 3]));
+          HIPCHK(hipEventElapsedTime(&kr, ev[(size_t)4 * c], ev[(size_t)4 * c + 1]));
+          HIPCHK(hipEventElapsedTime(&kc, ev[(size_t)4 * c + 2], ev[(size_t)4 * c + 3]));
           km += kr;
           kg += kc;
         }
         row_ms += km;
         gram_ms += kg;
-      } else if (nch > 0) {  // chunked procedural pass: the row kernels' spans, the rest is Gram
-        for (int c = 0; c < nch; ++c) {
-          float kc = 0.f;
-          HIPCHK(hipEventElapsedTime(&kc, evch[(size_t)2 * c], evch[(size_t)2 * c + 1]));
-          km += kc;
-        }
       } else {
         HIPCHK(hipEventElapsedTime(&km, ev0, evm));
-      }
-      if (nov == 0) {
         row_ms += km;
         gram_ms += k1 - km;
       }
@@ -895,17 +910,29 @@ struct sglm_engine : public Backend {
       g.nb_lim = INT64_MAX;
       if (nch > 0) {  // procedural shard in chunks: generate C rows into the scratch, resident Gram over it
         const int64_t plen = packed_len(p);
-        g.X = dxsc;
+        const int64_t bufd = ch_rows * (int64_t)g.ncols;  // doubles per scratch buffer
         g.ld = ch_rows;
         g.proc = ProcX{};
-        r.xs_out = dev_only ? nullptr : dxsc;  // deviance only: eta from the generator, no scratch
         r.xs_ld = ch_rows;
+        hipStream_t rs = proc_ov ? st2 : st;  // row kernels
+        if (proc_ov) {
+          HIPCHK(hipEventRecord(evch[(size_t)4 * nch], st));  // fork: beta uploaded, the last pass done
+          HIPCHK(hipStreamWaitEvent(st2, evch[(size_t)4 * nch], 0));
+        }
         for (int c = 0; c < nch; ++c) {
+          double* xs = dxsc + (proc_ov ? (int64_t)(c & 1) * bufd : 0);
           r.r_begin = (int64_t)c * ch_rows;
           r.r_end = r.r_begin + ch_rows;
-          HIPCHK(hipEventRecord(evch[(size_t)2 * c], st));
-          HIPCHK(launch_wide_rows(r, rgrid, st));
-          HIPCHK(hipEventRecord(evch[(size_t)2 * c + 1], st));
+          r.xs_out = dev_only ? nullptr : xs;  // deviance only: eta from the generator, no scratch
+          r.row_partials = proc_ov ? rowpart(c) : drp;
+          // buffer c & 1 is free once the Gram kernels of chunk c - 2 are done with it
+          if (proc_ov && c >= 2) HIPCHK(hipStreamWaitEvent(st2, evch[(size_t)4 * (c - 2) + 3], 0));
+          HIPCHK(hipEventRecord(evch[(size_t)4 * c], rs));
+          HIPCHK(launch_wide_rows(r, proc_ov && c > 0 ? rgrid_ov : rgrid, rs, proc_ov && c > 0));
+          HIPCHK(hipEventRecord(evch[(size_t)4 * c + 1], rs));
+          if (proc_ov) HIPCHK(hipStreamWaitEvent(st, evch[(size_t)4 * c + 1], 0));
+          HIPCHK(hipEventRecord(evch[(size_t)4 * c + 2], st));
+          g.X = xs;
           g.w = dw + r.r_begin;
           g.wz = dwz + r.r_begin;
           for (int kind = 0; kind < 2 && !dev_only; ++kind) {
@@ -914,7 +941,9 @@ struct sglm_engine : public Backend {
             g.wg_begin = dwgb[kind];
             HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
           }
-          HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dchunks + (int64_t)c * plen, st));
+          HIPCHK(hipEventRecord(evch[(size_t)4 * c + 3], st));
+          HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, r.row_partials, proc_ov && c > 0 ? rgrid_ov : rgrid,
+                                    dchunks + (int64_t)c * plen, st));
         }
         HIPCHK(hipEventRecord(evm, st));  // unused in chunked timing (pass_timing sums evch)
         HIPCHK(hipEventRecord(ev1, st));
@@ -928,7 +957,6 @@ struct sglm_engine : public Backend {
           r0 = (int64_t)c * ov_rows;
           r1 = std::min<int64_t>(n_pad, r0 + ov_rows);
         };
-        auto rowpart = [&](int c) { return drp + (c == 0 ? 0 : ((int64_t)rgrid + (int64_t)(c - 1) * rgrid_ov) * NS); };
         HIPCHK(hipEventRecord(evov[(size_t)4 * nov], st));  // fork: beta uploaded, the last pass's Gram done
         HIPCHK(hipStreamWaitEvent(st2, evov[(size_t)4 * nov], 0));
         for (int c = 0; c < nov; ++c) {
@@ -1336,6 +1364,8 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
+  if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
+  if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
   if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
   if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
@@ -1766,7 +1796,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
     out->ndev = (int)h->subs.size();
     out->rccl_group = h->gcomms.empty() ? 0 : 1;
     out->dev_passes = h->dev_passes;
-    out->overlap_chunks = h->subs.empty() ? 0 : h->subs[0]->nov;
+    out->overlap_chunks = h->subs.empty() ? 0 : h->subs[0]->ov_chunks();
     return SGLM_OK;
   }
   out->passes = h->passes;
@@ -1788,7 +1818,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->ndev = 1;
   out->rccl_group = 0;
   out->dev_passes = h->dev_passes;
-  out->overlap_chunks = h->nov;
+  out->overlap_chunks = h->ov_chunks();
   return SGLM_OK;
 }
 

@@ -113,3 +113,47 @@ def test_overlapped_lm_and_timing_split(engines):
     assert rel(f.coefs, r["coefs"]) < TOL and rel(f.stderr, r["stderr"]) < TOL
     st = e3.stats()
     assert st["row_kernel_ms"] > 0 and st["gram_kernel_ms"] > 0
+
+
+def _proc_engine(chunks: int, spec: bool = True) -> Engine:
+    env = {"SGLM_PROC_OVERLAP": str(chunks), "SGLM_PROC_OV_MIN": "4096", "SGLM_SPECULATE": "1" if spec else "0",
+           "SGLM_WIDE_OVERLAP": "1"}
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Engine(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("kind,p,fam,link", [(0, 520, "binomial", "logit"), (2, 300, "poisson", "log")])
+def test_overlapped_procedural_chunks(kind, p, fam, link):
+    """Procedural shards (X generated per pass into an HBM scratch, configs[4]'s path) with two
+    scratch buffers: the row kernel of chunk c + 1 generates while the Gram kernels of chunk c read.
+    Equal to the resident fit to rounding (another chunking), bitwise run to run and with the
+    deviance-only last pass."""
+    n = 30000
+    ov, ov2, res = _proc_engine(6), _proc_engine(6, spec=False), _engine(1)
+    try:
+        ov.synth(kind, 77, n, p, 3, procedural=True)
+        assert ov.stats()["overlap_chunks"] == 6
+        a = ov.fit_glm(fam, link)
+        b = ov.fit_glm(fam, link)
+        ov2.synth(kind, 77, n, p, 3, procedural=True)
+        c = ov2.fit_glm(fam, link)
+        res.synth(kind, 77, n, p, 3)
+        r = res.fit_glm(fam, link)
+    finally:
+        for e in (ov, ov2, res):
+            e.close()
+    np.testing.assert_array_equal(a.coefs, b.coefs)
+    np.testing.assert_array_equal(a.coefs, c.coefs)
+    np.testing.assert_array_equal(a.stderr, c.stderr)
+    assert (a.deviance, a.pearson, a.loglik, a.iter) == (c.deviance, c.pearson, c.loglik, c.iter)
+    assert a.iter == r.iter
+    d = (rel(a.coefs, r.coefs), rel(a.stderr, r.stderr), rel([a.deviance, a.pearson], [r.deviance, r.pearson]))
+    assert max(d) < 1e-11, d

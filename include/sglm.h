@@ -217,6 +217,12 @@ int sglm_fit_lm(sglm_engine *h, sglm_prelm *out);
 int sglm_irls_pass(sglm_engine *h, const sglm_glm_opts *opts, const double *beta, double mu0,
                    double *gram, double *xtwz, double *scalars);
 
+/* The test-level step of SURVEY.md 8(b): the pass at beta (beta != NULL) with the deviance at
+ * beta (family factor applied, as GLM.scala:397 createBinomialDeviance sums it).  Outputs may be
+ * NULL: xtwx [p*p] col-major full symmetric X'WX, xtwz [p], dev. */
+int sglm_irls_step(sglm_engine *h, const sglm_glm_opts *opts, const double *beta, double *xtwx, double *xtwz,
+                   double *dev);
+
 /* `iters` IRLS iterations from beta (in/out): each is one fused pass at beta followed by
  * the p x p solve -- the unit the benchmark times.  last_dev (may be NULL) receives the
  * deviance at the last input beta. */

@@ -25,7 +25,7 @@ S_DEV, S_PEARSON, S_LL, S_BAD, S_AUX0, S_AUX1, S_AUX2, S_SUMW = range(8)
 EXPORTS = [
     "sglm_abi_version", "sglm_last_error", "sglm_device_count", "sglm_create", "sglm_destroy",
     "sglm_set_data", "sglm_set_data_device", "sglm_synth", "sglm_synth_procedural", "sglm_get_data", "sglm_set_comm",
-    "sglm_rccl_unique_id", "sglm_set_comm_rccl", "sglm_fit_glm", "sglm_fit_lm", "sglm_irls_pass",
+    "sglm_rccl_unique_id", "sglm_set_comm_rccl", "sglm_fit_glm", "sglm_fit_lm", "sglm_irls_pass", "sglm_irls_step",
     "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
     "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
@@ -124,6 +124,7 @@ def load():
         "sglm_fit_glm": ([h, C.POINTER(GlmOpts), C.POINTER(PreGLM)], C.c_int),
         "sglm_fit_lm": ([h, C.POINTER(PreLM)], C.c_int),
         "sglm_irls_pass": ([h, C.POINTER(GlmOpts), dp, C.c_double, dp, dp, dp], C.c_int),
+        "sglm_irls_step": ([h, C.POINTER(GlmOpts), dp, dp, dp, dp], C.c_int),
         "sglm_irls_iterations": ([h, C.POINTER(GlmOpts), dp, C.c_int, dp], C.c_int),
         "sglm_predict": ([h, dp, C.c_int, dp], C.c_int),
         "sglm_get_stats": ([h, C.POINTER(Stats)], C.c_int),

@@ -1711,6 +1711,18 @@ int sglm_irls_pass(sglm_engine* h, const sglm_glm_opts* opts, const double* beta
   return SGLM_OK;
 }
 
+int sglm_irls_step(sglm_engine* h, const sglm_glm_opts* opts, const double* beta, double* xtwx, double* xtwz,
+                   double* dev) {
+  if (!beta) {
+    set_error("requirement failed: beta");
+    return SGLM_EINVAL;
+  }
+  double s[NS];
+  if (int rc = sglm_irls_pass(h, opts, beta, 0.0, xtwx, xtwz, s)) return rc;
+  if (dev) *dev = family_dev_factor(opts->family) * s[S_DEV];
+  return SGLM_OK;
+}
+
 int sglm_irls_iterations(sglm_engine* h, const sglm_glm_opts* opts, double* beta, int iters, double* last_dev) {
   if (int rc = check_handle(h)) return rc;
   if (!opts || !beta || iters < 0) {

@@ -238,6 +238,16 @@ class Engine:
                                          L.ptr(xtwz), L.ptr(s)), "sglm_irls_pass")
         return gram, xtwz, s
 
+    def irls_step(self, beta, family="binomial", link="logit"):
+        """SURVEY 8(b)'s test-level step: X'WX, X'Wz and the deviance at beta."""
+        o = glm_opts(family, link)
+        p = self.p
+        xtwx, xtwz, dev = np.zeros((p, p), order="F"), np.zeros(p), C.c_double()
+        b = np.ascontiguousarray(beta, dtype=np.float64)
+        L.check(self._lib.sglm_irls_step(self._h, C.byref(o), L.ptr(b), xtwx.ctypes.data_as(L.dp), L.ptr(xtwz),
+                                         C.byref(dev)), "sglm_irls_step")
+        return xtwx, xtwz, dev.value
+
     def irls_iterations(self, beta, iters, family="binomial", link="logit"):
         o = glm_opts(family, link)
         b = np.ascontiguousarray(beta, dtype=np.float64).copy()

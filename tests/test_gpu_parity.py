@@ -75,6 +75,11 @@ def test_pass_gram_every_kernel_variant(eng, p):
     assert nrel(xz, X.T @ (w * z)) < 1e-13
     dev = np.sum(y * np.log(np.maximum(y, 1) / mu) + (1 - y) * np.log(np.maximum(1 - y, 1) / (1 - mu)))
     assert rel(s[0], dev) < 1e-12
+    # SURVEY 8(b)'s test-level step: the same pass, deviance with createBinomialDeviance's factor 2
+    G2, xz2, d2 = eng.irls_step(beta)
+    np.testing.assert_array_equal(G2, G)
+    np.testing.assert_array_equal(xz2, xz)
+    assert d2 == 2.0 * s[0]
 
 
 @pytest.mark.parametrize("p,link", [(3, "logit"), (40, "probit"), (64, "cloglog"), (130, "logit"), (256, "logit")])

@@ -122,10 +122,6 @@ struct WideGramArgs {
   int dbg;              // profiling ablations: 4 DMA, 32 barriers
   ProcX proc;
   int64_t nb_lim;       // blocks of this launch's rows: pieces are clipped to [b0, min(b1, nb_lim))
-  unsigned* pace;       // banded pieces: per-epoch finished counters (zeroed per launch), or null
-  int pace_need;        // banded workgroups of the launch
-  int pace_ep;          // steps per epoch
-  int pace_lag;         // epochs a workgroup may run ahead of the slowest
 };
 
 // Arguments of the final-statistics pass (stats_kernel).

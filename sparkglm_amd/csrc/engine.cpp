@@ -164,14 +164,6 @@ struct sglm_engine : public Backend {
   int* dwgb[2] = {nullptr, nullptr};
   int* dstr = nullptr;                          // [nst][2] partial slot range per super-tile
   bool has_sched[2] = {false, false};
-  // pace of the banded schedules (wide.hip pace_step): per kind, the banded workgroups, steps
-  // per epoch and counter words; one counter array, zeroed before each Gram launch
-  bool allow_pace = true;  // SGLM_WIDE_PACE=0 disables
-  int pace_need[2] = {0, 0}, pace_ep[2] = {1, 1};
-  int64_t pace_words[2] = {0, 0};
-  static constexpr int PACE_LAG = 4;
-  unsigned* dpace = nullptr;
-  int64_t pace_cap = 0;
   hipEvent_t evm = nullptr;
   rocblas_handle blas = nullptr;
   // stats
@@ -238,9 +230,6 @@ struct sglm_engine : public Backend {
       evstage[k] = nullptr;
     }
     free_schedule();
-    if (dpace) (void)hipFree(dpace);
-    dpace = nullptr;
-    pace_cap = 0;
     part_cap = red_cap = gp_cap = rp_cap = 0;
     if (blas) (void)rocblas_destroy_handle(blas);
     blas = nullptr;
@@ -319,7 +308,6 @@ struct sglm_engine : public Backend {
 
   void free_schedule() {
     for (int k = 0; k < 2; ++k) {
-      pace_words[k] = 0;
       if (dpieces[k]) (void)hipFree(dpieces[k]);
       if (dwgb[k]) (void)hipFree(dwgb[k]);
       dpieces[k] = nullptr;
@@ -363,13 +351,6 @@ struct sglm_engine : public Backend {
       if (banded_kind((int)sts.size(), nb, G)) {
         const int S = (int)sts.size();
         const int k = G / S, E = G - S * k;
-        if (allow_pace) {  // epoch = the steps that keep ~96 MiB of rows in flight over LAG + 1 epochs
-          const int64_t step_bytes = (int64_t)k * WIDE_RB * ((p + 7) / 8 * 8) * (int64_t)sizeof(double);
-          const int64_t window = std::max<int64_t>(4, ((int64_t)96 << 20) / step_bytes);
-          pace_need[kind] = S * k;
-          pace_ep[kind] = (int)std::max<int64_t>(1, window / (PACE_LAG + 1));
-          pace_words[kind] = ((nb + k - 1) / k + pace_ep[kind] - 1) / pace_ep[kind] + 1;
-        }
         const int64_t tail = nb * E / G, nbm = nb - tail;  // banded blocks [0, nbm), tail [nbm, nb)
         const int per_xcd = std::max(1, G / 8);
         std::vector<int> gq((size_t)S * k), extra;  // pair q = j S + s -> workgroup; the left-over workgroups
@@ -431,12 +412,6 @@ struct sglm_engine : public Backend {
         }
         wgb[(size_t)G] = (int)pieces.size();
       }
-      if (pace_words[kind] > pace_cap) {
-        if (dpace) HIPCHK(hipFree(dpace));
-        dpace = nullptr;
-        pace_cap = (pace_words[kind] + 3) / 4 * 4;
-        HIPCHK(hipMalloc(&dpace, sizeof(unsigned) * (size_t)pace_cap));
-      }
       HIPCHK(hipMalloc(&dpieces[kind], sizeof(WidePiece) * pieces.size()));
       HIPCHK(hipMalloc(&dwgb[kind], sizeof(int) * wgb.size()));
       HIPCHK(hipMemcpy(dpieces[kind], pieces.data(), sizeof(WidePiece) * pieces.size(), hipMemcpyHostToDevice));
@@ -452,24 +427,6 @@ struct sglm_engine : public Backend {
   // chunks whose row kernels run beside the Gram (resident or procedural), 0 if none
   int ov_chunks() const { return nov > 1 ? nov : (proc_ov ? nch : 0); }
   double* rowpart(int c) const { return drp + (c == 0 ? 0 : ((int64_t)rgrid + (int64_t)(c - 1) * rgrid_ov) * NS); }
-
-  // One Gram launch of kind (0 off-diagonal, 1 diagonal super-tiles) over g's rows, paced when
-  // its schedule is banded and X is resident (or a chunk scratch).
-  int gram_launch(WideGramArgs& g, int kind) {
-    if (!has_sched[kind]) return SGLM_OK;
-    g.pieces = dpieces[kind];
-    g.wg_begin = dwgb[kind];
-    g.pace = nullptr;
-    if (pace_words[kind] > 0 && !g.proc.on) {
-      HIPCHK(hipMemsetAsync(dpace, 0, (size_t)(pace_words[kind] + 3) / 4 * 16, st));
-      g.pace = dpace;
-      g.pace_need = pace_need[kind];
-      g.pace_ep = pace_ep[kind];
-      g.pace_lag = PACE_LAG;
-    }
-    HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
-    return SGLM_OK;
-  }
 
   int ensure_wide_workspace() {
     npan = wide_panels((int)p);
@@ -978,8 +935,12 @@ struct sglm_engine : public Backend {
           g.X = xs;
           g.w = dw + r.r_begin;
           g.wz = dwz + r.r_begin;
-          for (int kind = 0; kind < 2 && !dev_only; ++kind)
-            if (int rc = gram_launch(g, kind)) return rc;
+          for (int kind = 0; kind < 2 && !dev_only; ++kind) {
+            if (!has_sched[kind]) continue;
+            g.pieces = dpieces[kind];
+            g.wg_begin = dwgb[kind];
+            HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+          }
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 3], st));
           HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, r.row_partials, proc_ov && c > 0 ? rgrid_ov : rgrid,
                                     dchunks + (int64_t)c * plen, st));
@@ -1014,8 +975,12 @@ struct sglm_engine : public Backend {
           g.w = dw + r0;
           g.wz = dwz + r0;
           g.nb_lim = (r1 - r0) / WIDE_RB;
-          for (int kind = 0; kind < 2 && !dev_only; ++kind)
-            if (int rc = gram_launch(g, kind)) return rc;
+          for (int kind = 0; kind < 2 && !dev_only; ++kind) {
+            if (!has_sched[kind]) continue;
+            g.pieces = dpieces[kind];
+            g.wg_begin = dwgb[kind];
+            HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+          }
           HIPCHK(hipEventRecord(evov[(size_t)4 * c + 3], st));
           HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, rowpart(c), c == 0 ? rgrid : rgrid_ov,
                                     dchunks + (int64_t)c * plen, st));
@@ -1027,8 +992,12 @@ struct sglm_engine : public Backend {
       }
       HIPCHK(launch_wide_rows(r, rgrid, st));
       HIPCHK(hipEventRecord(evm, st));
-      for (int kind = 0; kind < 2 && !dev_only; ++kind)
-        if (int rc = gram_launch(g, kind)) return rc;
+      for (int kind = 0; kind < 2 && !dev_only; ++kind) {
+        if (!has_sched[kind]) continue;
+        g.pieces = dpieces[kind];
+        g.wg_begin = dwgb[kind];
+        HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+      }
       HIPCHK(hipEventRecord(ev1, st));
       HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dred, st));
     } else {
@@ -1399,7 +1368,6 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
   if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
-  if (const char* wp = std::getenv("SGLM_WIDE_PACE")) h->allow_pace = std::atoi(wp) != 0;
   if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;

@@ -266,43 +266,6 @@ __device__ __forceinline__ void diag_block(const double* lds, int buf, int lane,
   }
 }
 
-// Pace of the banded schedule (a.pace != null, pieces with block stride > 1): the workgroups of
-// a launch sweep the same rows so that a block one super-tile fetches is re-read from the
-// Infinity Cache by the others -- but only while they stay close.  Unpaced, they drift apart
-// over a long launch (p = 2048: 12.6x the algorithmic X traffic).  Every pace_ep steps wave 0
-// of a banded workgroup adds one to the finished epoch's counter and, before starting epoch e,
-// waits until all pace_need banded workgroups finished epoch e - pace_lag.  Timing only: no
-// data passes through the counters, so the relaxed agent-scope atomics need no release /
-// acquire, and the spin is bounded (a workgroup that waited PACE_SPINS polls goes on) -- the
-// launch cannot hang on a workgroup that is not resident.  The other waves wait at the block
-// barrier that follows.
-#ifndef PACE_SPINS
-#define PACE_SPINS 256
-#endif
-__device__ __forceinline__ void pace_step(const WideGramArgs& a, bool on, int64_t t, int wv, int lane) {
-  if (!on || wv != 0 || (t % a.pace_ep) != 0) return;
-  const int64_t e = t / a.pace_ep;
-  if (lane == 0) {
-    if (e > 0) __hip_atomic_fetch_add(a.pace + (e - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e >= a.pace_lag) {
-      unsigned* w = a.pace + (e - a.pace_lag);
-      for (int k = 0; k < PACE_SPINS && __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                                             (unsigned)a.pace_need; ++k)
-        __builtin_amdgcn_s_sleep(8);
-    }
-  }
-}
-// End of a banded piece: count this workgroup as done for every epoch it has not counted yet
-// (the pieces of a launch differ by one step at most), so nobody waits for it.
-__device__ __forceinline__ void pace_end(const WideGramArgs& a, bool on, int64_t b0, int64_t b1, int64_t bs, int wv,
-                                         int lane) {
-  if (!on || wv != 0 || lane != 0) return;
-  const int64_t steps = b0 < b1 ? (b1 - b0 + bs - 1) / bs : 0;
-  const int64_t nep = ((b1 + bs - 1) / bs + a.pace_ep - 1) / a.pace_ep;  // the longest piece (b0 = 0)
-  for (int64_t e = steps > 0 ? (steps - 1) / a.pace_ep : 0; e < nep; ++e)
-    __hip_atomic_fetch_add(a.pace + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Pipeline per piece (two LDS buffers, one barrier per block):
 //   wait for this wave's DMA of block blk; barrier (every wave's DMA of blk has landed and
 //   every wave is done reading the other buffer); DMA block blk+1 into the other buffer;
@@ -318,17 +281,14 @@ __device__ void diag_piece(double* lds, const WideGramArgs& a, int I, int64_t b0
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   int cur = 0;
-  const bool paced = a.pace && bs > 1;
   if (b0 < b1) wstage_diag<PROC>(lds, 0, a, b0, I, wv, loff, lane);
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
-    pace_step(a, paced, (blk - b0) / bs, wv, lane);
     wait_vm<0>();
     lds_bar();
     if (blk + bs < b1) wstage_diag<PROC>(lds, cur ^ 1, a, blk + bs, I, wv, loff, lane);
     diag_block<Q>(lds, cur, lane, acc, xz_lo, xz_hi);
   }
-  pace_end(a, paced, b0, b1, bs, wv, lane);
   constexpr int LO = Q, HI = PT - 1 - Q;
 #pragma unroll
   for (int k = 0; k <= PT; ++k) {
@@ -358,11 +318,9 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   lane_offsets(a, lane, loff);
   if (b0 < b1) wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
   int cur = 0;
-  const bool paced = a.pace && bs > 1;
 #pragma unroll 1
   for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
     const int64_t nb = blk + bs;
-    pace_step(a, paced, (blk - b0) / bs, wv, lane);
     wait_vm<0>();
     if (!(dbg & 32)) lds_bar();
     const bool next = nb < b1 && (!(dbg & 4) || blk == b0);
@@ -387,7 +345,6 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
       offdiag_block(lds, cur, wv, lane, acc, [](int) {});
     }
   }
-  pace_end(a, paced, b0, b1, bs, wv, lane);
   const int tr0 = 4 * (wv >> 1), tc0 = 4 * (wv & 1);
 #pragma unroll
   for (int t = 0; t < 4; ++t)

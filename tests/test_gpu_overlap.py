@@ -157,30 +157,3 @@ def test_overlapped_procedural_chunks(kind, p, fam, link):
     assert a.iter == r.iter
     d = (rel(a.coefs, r.coefs), rel(a.stderr, r.stderr), rel([a.deviance, a.pearson], [r.deviance, r.pearson]))
     assert max(d) < 1e-11, d
-
-
-def test_paced_banded_schedule_is_bitwise_unpaced():
-    """The pace of the banded Gram schedule (wide.hip pace_step: relaxed per-epoch counters,
-    bounded spins) only changes WHEN a workgroup runs a block, never what it sums or in which
-    order: paced and unpaced fits are bitwise identical, with and without overlapped chunks."""
-    fits = []
-    for pace in ("1", "0"):
-        saved = os.environ.get("SGLM_WIDE_PACE")
-        os.environ["SGLM_WIDE_PACE"] = pace
-        try:
-            for ov in (3, 1):
-                e = _engine(ov)
-                try:
-                    e.synth(0, 0, 40000, 640, 13)
-                    fits.append(e.fit_glm("binomial", "logit"))
-                finally:
-                    e.close()
-        finally:
-            if saved is None:
-                os.environ.pop("SGLM_WIDE_PACE", None)
-            else:
-                os.environ["SGLM_WIDE_PACE"] = saved
-    for a, b in ((fits[0], fits[2]), (fits[1], fits[3])):
-        np.testing.assert_array_equal(a.coefs, b.coefs)
-        np.testing.assert_array_equal(a.stderr, b.stderr)
-        assert (a.deviance, a.iter) == (b.deviance, b.iter)

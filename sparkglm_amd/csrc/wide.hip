@@ -35,12 +35,6 @@
 #ifndef WIDE_DIAG_WG
 #define WIDE_DIAG_WG 2
 #endif
-#ifndef WIDE_GRAM_PRIO
-#define WIDE_GRAM_PRIO 0
-#endif
-#ifndef WIDE_GRAM_PRIO_KIND
-#define WIDE_GRAM_PRIO_KIND 3
-#endif
 #ifndef WIDE_DIAG_BATCH
 #define WIDE_DIAG_BATCH 0  // diagonal k-steps: operands and VALU of the whole block before its MFMAs
 #endif
@@ -364,8 +358,6 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
 template <bool DIAG, bool PROC>
 __global__ void __launch_bounds__(64 * NWAVE, DIAG ? WIDE_DIAG_WG : 2) wide_gram_kernel(WideGramArgs a) {
   __shared__ double lds[DIAG ? LDS_DIAG : LDS_DOUBLES];
-  // issue priority ahead of an overlapped row kernel's waves (WIDE_GRAM_PRIO_KIND: 1 off-diagonal, 2 diagonal, 3 both)
-  if (WIDE_GRAM_PRIO && (WIDE_GRAM_PRIO_KIND & (DIAG ? 2 : 1))) __builtin_amdgcn_s_setprio(WIDE_GRAM_PRIO);
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pb = a.wg_begin[blockIdx.x], pe = a.wg_begin[blockIdx.x + 1];

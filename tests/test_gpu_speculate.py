@@ -96,3 +96,25 @@ def test_multi_device_handle_speculates_identically():
         off.close()
     assert k0 == 0
     _same(f1, f0)
+
+
+@pytest.mark.parametrize("max_iter", [1, 2, 0])
+def test_final_statistics_when_the_last_pass_was_not_predicted(max_iter):
+    """Narrow binomial/logit passes without m carry pearsonCalc / llBinomial only in the pass
+    predicted to end the fit (the others run without statistics and without an eta store).  A fit
+    that stops on a pass that was not predicted (here: max_iter 1 or 2, before any prediction is
+    possible) takes one deviance-only pass with statistics at the final beta -- bitwise the numbers
+    the every-pass-statistics engine (speculation off) reports."""
+    on, off = _engine(True), _engine(False)
+    try:
+        res = []
+        for e in (on, off):
+            e.synth(0, 0, 300_000, 32, 5)
+            e.reset_stats()
+            res.append((e.fit_glm("binomial", "logit", max_iter=max_iter), e.stats()["dev_passes"]))
+    finally:
+        on.close()
+        off.close()
+    (f1, k1), (f0, k0) = res
+    assert k0 == 0 and (k1 == 0 if max_iter else k1 >= 1)
+    _same(f1, f0)

@@ -120,12 +120,6 @@ struct sglm_engine : public Backend {
   Comm comm;
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
-  // Narrow binomial/logit passes without m carry the final statistics in their scalars instead of
-  // an eta store + stats_kernel (stats_lean).  Only the pass that ends a fit needs them: the
-  // speculative (predicted-last) pass, or every pass when speculation is off; the others run the
-  // leaner kernel (no statistics, no eta store).  A fit that converges on a pass without them
-  // (prediction missed) gets one deviance-only pass with statistics at the same beta (stats()).
-  bool stats_now = false;
   bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
   // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
   // scalar reduction but no Gram -- bitwise the scalars of the full pass.  SGLM_SPECULATE=0 off.
@@ -263,9 +257,6 @@ struct sglm_engine : public Backend {
 
   int64_t ncols() const override { return group() ? subs[0]->p : p; }
   bool pass_has_stats() const override { return group() ? subs[0]->lp_stats : lp_stats; }
-  bool stats_lean(int mode, int family, int link) const {
-    return narrow && mode == MODE_IRLS && family == FAM_BINOMIAL && link == LNK_LOGIT && !dm && !force_eta_store;
-  }
   int npart() const override { return group() ? (int)subs.size() : comm.nranks; }
 
   // ---- communicator helpers ----
@@ -875,10 +866,10 @@ struct sglm_engine : public Backend {
     a.partials = dpart;
     a.stride = stride;
     // binomial / logit (m = 1) on the narrow path: final statistics in the pass, no eta store
-    const bool lean = stats_lean(mode, family, link);
-    a.stats_in_pass = (lean && (dev_only || stats_now || !allow_spec)) ? 1 : 0;
+    a.stats_in_pass = (narrow && mode == MODE_IRLS && family == FAM_BINOMIAL && link == LNK_LOGIT && !dm &&
+                       !force_eta_store) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
-    a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !lean) ? deta : nullptr;
+    a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
@@ -1097,15 +1088,6 @@ struct sglm_engine : public Backend {
       return SGLM_OK;
     }
     HIPCHK(hipSetDevice(device));
-    if (stats_lean(mode, family, link)) {  // no eta store: a deviance-only pass with statistics at beta
-      std::vector<double> pk((size_t)packed_len(p));
-      stats_now = dev_only = true;
-      const int rc = pass(mode, beta, mu0, ybar, family, link, pk.data());  // all-reduced like any pass
-      stats_now = dev_only = false;
-      if (rc) return rc;
-      std::memcpy(s, pk.data() + tri_count(p) + p, sizeof(double) * NS);
-      return SGLM_OK;
-    }
     if (mode == MODE_LM_RESID) {  // pred = X * coefs into the eta buffer
       std::memcpy(hbeta, beta, sizeof(double) * p);
       HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * p, hipMemcpyHostToDevice, st));

@@ -99,12 +99,10 @@ def test_multi_device_handle_speculates_identically():
 
 
 @pytest.mark.parametrize("max_iter", [1, 2, 0])
-def test_final_statistics_when_the_last_pass_was_not_predicted(max_iter):
-    """Narrow binomial/logit passes without m carry pearsonCalc / llBinomial only in the pass
-    predicted to end the fit (the others run without statistics and without an eta store).  A fit
-    that stops on a pass that was not predicted (here: max_iter 1 or 2, before any prediction is
-    possible) takes one deviance-only pass with statistics at the final beta -- bitwise the numbers
-    the every-pass-statistics engine (speculation off) reports."""
+def test_capped_fits_speculate_identically(max_iter):
+    """A fit stopped by max_iter (GLM.scala has no cap; the engine's option) before any prediction
+    is possible, or run to convergence, is bitwise the same with speculation on and off -- final
+    statistics included (narrow binomial/logit: carried in every pass's scalars)."""
     on, off = _engine(True), _engine(False)
     try:
         res = []

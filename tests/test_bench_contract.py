@@ -78,12 +78,13 @@ def test_launcher_runs_ranks_with_rank_environment(tmp_path):
     import subprocess
     import sys
     probe = tmp_path / "probe.py"
-    probe.write_text("import os, json\nprint(json.dumps({k: os.environ.get(k) for k in "
-                     "('RANK','LOCAL_RANK','WORLD_SIZE','MASTER_ADDR')}))\n")
+    # one file per rank: two ranks printing to one pipe can interleave their lines
+    probe.write_text("import os, json\nd = {k: os.environ.get(k) for k in ('RANK','LOCAL_RANK','WORLD_SIZE','MASTER_ADDR')}\n"
+                     f"open(os.path.join({str(tmp_path)!r}, 'rank' + d['RANK'] + '.json'), 'w').write(json.dumps(d))\n")
     cmd = bench.launch_cmd(2, [], bench._free_port())
     cmd[cmd.index(os.path.abspath(bench.__file__))] = str(probe)
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    envs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    envs = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in (0, 1)]
     assert sorted(e["RANK"] for e in envs) == ["0", "1"]
     assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)

@@ -152,9 +152,23 @@ def launch_ranks(gpus: int, argv) -> int:
     return rc
 
 
+# The one JSON line goes here; main() points it at the process's original stdout and sends fd 1
+# itself to stderr, so lines that libraries write to stdout (gloo's "[Gloo] Rank 0 is connected
+# ..." when ranks rehearse over gloo, runtime banners) cannot come before or into it.
+JSON_OUT = sys.stdout
+
+
+def _guard_stdout() -> None:
+    global JSON_OUT
+    sys.stdout.flush()
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main() -> int:
     if needs_launch(os.environ, _gpus_arg(sys.argv[1:])):
         return launch_ranks(_gpus_arg(sys.argv[1:]), sys.argv[1:])
+    _guard_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -328,7 +342,7 @@ def main() -> int:
         if rank == 0:
             out["strong_scaling_1b_logit"] = strong_1b_res
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=JSON_OUT, flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
@@ -496,7 +510,7 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
             out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=JSON_OUT, flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()

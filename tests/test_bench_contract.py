@@ -88,3 +88,17 @@ def test_launcher_runs_ranks_with_rank_environment(tmp_path):
     envs = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in (0, 1)]
     assert sorted(e["RANK"] for e in envs) == ["0", "1"]
     assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+
+
+def test_stdout_carries_only_the_json_line():
+    """Rank processes send fd 1 to stderr (gloo and runtimes print there) and keep the original
+    stdout for the one JSON line the driver parses."""
+    import subprocess
+    import sys
+    code = ("import os, sys, json; sys.path.insert(0, %r); import bench; bench._guard_stdout(); "
+            "os.write(1, b'[Gloo] Rank 0 is connected to 1 peer ranks.\\n'); print('log line'); "
+            "print(json.dumps({'metric': 'm'}), file=bench.JSON_OUT, flush=True)") % os.path.dirname(bench.__file__)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == ['{"metric": "m"}']
+    assert "[Gloo]" in out.stderr and "log line" in out.stderr

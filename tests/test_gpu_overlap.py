@@ -28,12 +28,12 @@ def nrel(a, b):
     return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
 
 
-def _engine(chunks: int, spec: bool = True) -> Engine:
+def _engine(chunks: int, spec: bool = True, devices=None) -> Engine:
     env = {"SGLM_WIDE_OVERLAP": str(chunks), "SGLM_WIDE_OV_MIN": "1024", "SGLM_SPECULATE": "1" if spec else "0"}
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        return Engine(0)
+        return Engine(devices=devices) if devices else Engine(0)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -157,3 +157,23 @@ def test_overlapped_procedural_chunks(kind, p, fam, link):
     assert a.iter == r.iter
     d = (rel(a.coefs, r.coefs), rel(a.stderr, r.stderr), rel([a.deviance, a.pearson], [r.deviance, r.pearson]))
     assert max(d) < 1e-11, d
+
+
+def test_overlapped_shards_of_a_multi_device_handle():
+    """One process over several devices (sglm_create_multi; here device 0 twice, host sums in
+    shard order): every shard's pass overlaps its own row chunks with its Gram chunks."""
+    g, one = _engine(3, devices=[0, 0]), _engine(1)
+    try:
+        g.synth(0, 0, 40000, 300, 17)
+        assert g.stats()["overlap_chunks"] == 3
+        f = g.fit_glm("binomial", "logit")
+        one.synth(0, 0, 40000, 300, 17)
+        r = one.fit_glm("binomial", "logit")
+    finally:
+        g.close()
+        one.close()
+    X, y, _, _ = synth.generate(0, 0, 40000, 300, 17)
+    o = po.fit_glm(X, y, "binomial", "logit", nthreads=8)
+    assert f.iter == o.iter == r.iter
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel(f.coefs, r.coefs) < 1e-11

@@ -177,3 +177,22 @@ def test_overlapped_shards_of_a_multi_device_handle():
     assert f.iter == o.iter == r.iter
     assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
     assert rel(f.coefs, r.coefs) < 1e-11
+
+
+def test_procedural_shards_of_a_multi_device_handle():
+    """configs[4]'s procedural path (X generated per pass, never stored) sharded over the devices
+    of one handle (here device 0 twice): the same fit as one device and as the oracle."""
+    g, one = Engine(devices=[0, 0]), Engine(0)
+    try:
+        g.synth(0, 0, 20000, 520, 3, procedural=True)
+        f = g.fit_glm("binomial", "logit")
+        one.synth(0, 0, 20000, 520, 3, procedural=True)
+        r = one.fit_glm("binomial", "logit")
+    finally:
+        g.close()
+        one.close()
+    X, y, _, _ = synth.generate(0, 0, 20000, 520, 3)
+    o = po.fit_glm(X, y, "binomial", "logit", nthreads=8)
+    assert f.iter == r.iter == o.iter
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel(f.coefs, r.coefs) < 1e-11 and rel([f.deviance], [r.deviance]) < 1e-12

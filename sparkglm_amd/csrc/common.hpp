@@ -129,7 +129,11 @@ struct StatsArgs {
   const double* y;
   const double* m;
   const double* prior;
-  const double* eta;    // MODE_IRLS: eta of the last pass; MODE_LM_RESID: X*coefs
+  const double* eta;    // MODE_IRLS: eta of the last pass; MODE_LM_RESID: X*coefs (or X != null below)
+  const double* X;      // MODE_LM_RESID on a resident shard: eta = X*beta formed in the kernel
+  int64_t ld;           //   (predict_kernel's order), so the residual pass reads X once and
+  int p;                //   writes no eta
+  const double* beta;
   int64_t n;
   int family, link, mode;
   double mu0, ybar;

@@ -1091,9 +1091,15 @@ struct sglm_engine : public Backend {
     if (mode == MODE_LM_RESID) {  // pred = X * coefs into the eta buffer
       std::memcpy(hbeta, beta, sizeof(double) * p);
       HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * p, hipMemcpyHostToDevice, st));
-      HIPCHK(launch_predict(dX, n_pad, (int)p, n, dbeta, nullptr, deta, st, procx));
+      if (procx.on) HIPCHK(launch_predict(dX, n_pad, (int)p, n, dbeta, nullptr, deta, st, procx));
     }
     StatsArgs a{};
+    if (mode == MODE_LM_RESID && !procx.on) {  // one read of X, no eta round trip
+      a.X = dX;
+      a.ld = n_pad;
+      a.p = (int)p;
+      a.beta = dbeta;
+    }
     a.y = dy;
     a.m = (mode == MODE_LM_RESID) ? nullptr : dm;
     a.prior = (mode == MODE_LM_RESID) ? nullptr : dprior;

@@ -570,7 +570,12 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const double m = a.m ? a.m[i] : 1.0;
     const double pw = a.prior ? a.prior[i] : 1.0;
-    const double eta = a.eta ? a.eta[i] : 0.0;
+    double eta = 0.0;
+    if (a.X) {  // LM residuals: X*coefs in predict_kernel's order (LM.scala:173-174)
+      for (int j = 0; j < a.p; ++j) eta += a.X[(int64_t)j * a.ld + i] * a.beta[j];
+    } else if (a.eta) {
+      eta = a.eta[i];
+    }
     stats_row(FAM, LNK, a.mode, eta, a.y[i], m, pw, a.mu0, a.ybar, a.m != nullptr, acc);
   }
 #pragma unroll

@@ -24,6 +24,8 @@ CASES = {
     "logit1b": (0, 0, 1_000_000_000, 32, 6, "binomial", "logit"),      # north-star strong-scaling fit
     "logit256": (0, 0, 100_000_000, 256, 2, "binomial", "logit"),      # BASELINE configs[1] (headline)
     "poisson64": (2, 0, 125_000_000, 64, 3, "poisson", "log"),         # configs[2] per-GPU shard
+    "logit512r": (0, 0, 60_000_000, 512, 5, "binomial", "logit"),      # configs[4] p, resident: the wide path
+    "gamma2048": (3, 0, 12_500_000, 2048, 4, "gamma", "inverse"),     # configs[3] per-GPU shard, wide + GPU solve
 }
 
 

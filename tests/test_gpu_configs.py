@@ -89,8 +89,9 @@ FULL = _full_scale()
 
 @pytest.mark.parametrize("name", sorted(FULL))
 def test_full_scale_fit_matches_streaming_oracle(eng, name):
-    """The bench workloads at their full sizes (1B x 32, 100M x 256, 125M x 64 + offset + prior),
-    generated in HBM, against the streaming oracle's fits of the same generator
+    """The bench workloads at their full sizes (1B x 32, 100M x 256, 125M x 64 + offset + prior,
+    and the wide ones: 60M x 512 logit -- overlapped row / Gram chunks -- and 12.5M x 2048 gamma
+    with the GPU solve), generated in HBM, against the streaming oracle's fits of the same generator
     (tests/golden/make_full_scale.py): GLM.scala:452-462's absolute tol 1e-6 on a deviance of
     up to ~1.3e9 decides the iteration count, so the final |delta deviance| is printed beside it."""
     c = FULL[name]
@@ -101,7 +102,9 @@ def test_full_scale_fit_matches_streaming_oracle(eng, name):
           f"{abs(f.dev_trace[-1] - f.dev_trace[-2]):.3e} oracle {abs(tr[-1] - tr[-2]):.3e} vs tol {c['tol']:.0e}; "
           f"previous {abs(f.dev_trace[-2] - f.dev_trace[-3]):.3e}")
     assert f.iter == c["iter"]
-    assert rel(f.coefs, c["coefs"]) < TOL and rel(f.stderr, c["stderr"]) < TOL
+    # gamma/inverse at p = 2048 is ill-conditioned: coefficients norm-wise
+    ec = nrel(f.coefs, c["coefs"]) if c["family"] == "gamma" else rel(f.coefs, c["coefs"])
+    assert ec < TOL and rel(f.stderr, c["stderr"]) < TOL, (ec, rel(f.stderr, c["stderr"]))
     assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
                [c["deviance"], c["null_deviance"], c["pearson"], c["loglik"]]) < TOL
     assert rel(f.dev_trace, tr) < TOL

@@ -315,6 +315,9 @@ def main() -> int:
             "roofline": roof,
             "breakdown_ms_per_step": {"pass_kernels": pass_ms,
                                       "row_kernel": st["row_kernel_ms"] / passes if wide else None,
+                                      # wide path: row kernels of chunks >= 1 run beside the Gram on a
+                                      # second stream, so row + Gram exceed the pass's wall span
+                                      "row_overlap_chunks": st["overlap_chunks"] if wide else None,
                                       "reduce": st["reduce_kernel_ms"] / passes,
                                       "solve": st["solve_ms"] / args.steps,
                                       "comm": st["comm_ms"] / args.steps},

@@ -254,6 +254,7 @@ def main() -> int:
     barrier()
     dt = time.perf_counter() - t0
     st = eng.stats()
+    ranks_diag = rank_stats(st, args.steps, dist_on, shared)
     if dist_on:
         tt = torch.tensor([dt, ttc], dtype=torch.float64, device="cpu" if shared else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -321,6 +322,8 @@ def main() -> int:
                                       "reduce": st["reduce_kernel_ms"] / passes,
                                       "solve": st["solve_ms"] / args.steps,
                                       "comm": st["comm_ms"] / args.steps},
+            "ranks": ranks_diag,
+            "solve_path": st["solve_path_name"],
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
@@ -328,14 +331,13 @@ def main() -> int:
         else:
             out["cpu_baseline"] = None
     eng.close()
-    if not args.no_load:
-        try:  # the H2D load of a host-resident design, reported apart from the fit
-            load = load_probe(dev, p, wl, n)
+    if not args.no_load and rank == 0:
+        try:  # the H2D load of a host-resident design, reported apart from the fit;
+            # rank 0 only (every rank would otherwise build ~4 GB of host arrays it throws away)
+            out["load"] = load_probe(dev, p, wl, n)
         except Exception as exc:
             log(f"[rank {rank}] load probe failed: {exc}")
-            load = None
-        if rank == 0:
-            out["load"] = load
+            out["load"] = None
     if args.workload == "logit256" and not args.no_strong:
         try:  # the north-star 1B-row strong-scaling point, beside the headline (own shard, freed after)
             strong_1b_res = strong_1b(args, dev, world, rank, dist_on, shared, barrier)
@@ -381,6 +383,28 @@ def load_probe(dev: int, p: int, wl: dict, n_shard: int, sample_bytes: float = 4
             else None}
 
 
+def rank_stats(st: dict, iters: int, dist_on: bool, shared: bool) -> dict:
+    """Per-rank diagnostics of a multi-GPU line (collective: every rank calls it): pass-kernel,
+    reduce-kernel and all-reduce ms per iteration as min and max over the ranks, the all-reduce
+    path and whether the scalars went through rank blocks -- enough to tell a compute straggler
+    (pass max >> min) from a slow collective (comm) when the scaling curve disappoints."""
+    import torch
+    import torch.distributed as dist
+    it = max(iters, 1)
+    v = [st["pass_kernel_ms"] / it, st["reduce_kernel_ms"] / it, st["comm_ms"] / it, st["solve_ms"] / it]
+    lo = torch.tensor(v, dtype=torch.float64, device="cpu" if (shared or not dist_on) else "cuda")
+    hi = lo.clone()
+    if dist_on:
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    lo, hi = lo.cpu().tolist(), hi.cpu().tolist()
+    names = ["pass_kernel_ms", "reduce_kernel_ms", "comm_ms", "solve_ms"]
+    out = {f"{k}_per_iter_{m}": (a if m == "min" else b) for k, a, b in zip(names, lo, hi) for m in ("min", "max")}
+    out["allreduce_path"] = st["comm_path_name"]
+    out["scalar_rank_blocks"] = bool(st["rank_blocks"])
+    return out
+
+
 def _gpus_arg(argv) -> int:
     ap = argparse.ArgumentParser(add_help=False)
     ap.add_argument("--gpus", type=int, default=1)
@@ -395,7 +419,7 @@ def attach_comm(eng, args, world: int, rank: int, dist_on: bool, shared: bool) -
     from sparkglm_amd import Engine
     if shared:
         from sparkglm_amd.distributed import torch_allreduce
-        eng.set_comm(torch_allreduce(), on_device=False)
+        eng.set_comm(torch_allreduce(), on_device=False, rank=rank)
     elif dist_on:
         comm = args.comm
         if comm == "rccl":  # the engine's own RCCL communicator (sglm_set_comm_rccl)
@@ -412,7 +436,7 @@ def attach_comm(eng, args, world: int, rank: int, dist_on: bool, shared: bool) -
                 comm = "torch"
         if comm != "rccl":
             from sparkglm_amd.distributed import torch_allreduce
-            eng.set_comm(torch_allreduce(), on_device=True)
+            eng.set_comm(torch_allreduce(), on_device=True, rank=rank)
         args.comm = comm
 
 
@@ -449,11 +473,13 @@ def strong_1b(args, dev: int, world: int, rank: int, dist_on: bool, shared: bool
         beta = np.array(fit.coefs, dtype=np.float64)
         beta, _ = eng.irls_iterations(beta, 1, wl["family"], wl["link"])
         k = 5
+        eng.reset_stats()
         barrier()
         t0 = time.perf_counter()
         eng.irls_iterations(beta, k, wl["family"], wl["link"])
         barrier()
         it_s = (time.perf_counter() - t0) / k
+        diag = rank_stats(eng.stats(), k, dist_on, shared)
     finally:
         eng.close()
     if dist_on:
@@ -462,7 +488,8 @@ def strong_1b(args, dev: int, world: int, rank: int, dist_on: bool, shared: bool
         ttc, it_s = float(tt[0]), float(tt[1])
     return {"workload": "logit1b: " + wl["label"], "global_rows": wl["strong_rows"], "p": wl["p"],
             "n_gpus": world, "scaling": "strong", "time_to_converge_s": ttc, "iters_to_converge": fit.iter,
-            "deviance": fit.deviance, "ms_per_iter": it_s * 1e3, "rows_per_s_per_iter": wl["strong_rows"] / it_s}
+            "deviance": fit.deviance, "ms_per_iter": it_s * 1e3, "rows_per_s_per_iter": wl["strong_rows"] / it_s,
+            "ranks": diag}
 
 
 def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:

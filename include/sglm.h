@@ -55,7 +55,9 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 4  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks */
+#define SGLM_ABI_VERSION 5  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
+                              sglm_stats.comm_path / rank_blocks / pass_kernel_ms_min / proc_chunks /
+                              proc_chunk_rows / solve_path */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -78,6 +80,24 @@ enum sglm_link {
 enum sglm_init {
   SGLM_INIT_SINGLE = 0,  /* fitSingleBinomial: mu = mean(y) directly (GLM.scala:263, 282-290) */
   SGLM_INIT_MULTIPLE = 1 /* fitMultipleBinomial: mu = unlink(link(mean(y))) (GLM.scala:370-371) */
+};
+
+/* How the last p x p solve ran (sglm_stats.solve_path). */
+enum sglm_solve_path {
+  SGLM_SOLVE_HOST_CHOL = 0,   /* host Cholesky (p <= 256, well conditioned) */
+  SGLM_SOLVE_HOST_LU = 1,     /* host LU + explicit inverse: Breeze inv (utils.scala:103-105) */
+  SGLM_SOLVE_DEVICE_CHOL = 2, /* wide p, SGLM_WIDE_SOLVE=chol: rocSOLVER potrf / potrs / potri */
+  SGLM_SOLVE_DEVICE_LU = 3    /* wide p (default): rocSOLVER getrf + getri, coefs = inv * X'Wz */
+};
+
+/* Where a pass's all-reduce ran (sglm_stats.comm_path). */
+enum sglm_comm_path {
+  SGLM_COMM_NONE = 0,         /* one shard, no communicator */
+  SGLM_COMM_CALLER_HOST = 1,  /* sglm_set_comm, host buffers (gloo, sglm_local_allreduce, ...) */
+  SGLM_COMM_CALLER_DEVICE = 2,/* sglm_set_comm, device buffers (e.g. a torch RCCL group) */
+  SGLM_COMM_RCCL = 3,         /* sglm_set_comm_rccl: the engine's own RCCL communicator (xGMI) */
+  SGLM_COMM_GROUP_RCCL = 4,   /* multi-device handle: one RCCL group call over ncclCommInitAll */
+  SGLM_COMM_GROUP_HOST = 5    /* multi-device handle with a repeated device: host sums in shard order */
 };
 
 /* Prediction scale (R's predict(type = "link" | "response")). */
@@ -147,6 +167,16 @@ typedef struct {
   int overlap_chunks;       /* wide path, resident X: chunks per pass whose row kernel runs on a
                                second stream beside the previous chunk's Gram (0: not overlapped;
                                SGLM_WIDE_OVERLAP sets the count, SGLM_WIDE_OV_MIN the fewest rows) */
+  int comm_path;            /* enum sglm_comm_path */
+  int rank_blocks;          /* 1: the scalars (deviance, ...) are summed across ranks / shards in rank
+                               order with compensation from per-rank blocks (needs the own rank: RCCL,
+                               the in-process communicator, or sglm_set_comm_rank); 0: plain sum */
+  double pass_kernel_ms_min;/* multi-device handle: pass_kernel_ms of the fastest shard (the max is
+                               pass_kernel_ms); one device: = pass_kernel_ms.  comm_ms there is
+                               the collective after the last shard arrived (RCCL: device events) */
+  int proc_chunks;          /* procedural shard: chunks of X generated per pass (0: in-kernel) */
+  int64_t proc_chunk_rows;  /* rows per chunk (SGLM_PROC_SCRATCH_MAX caps the scratch, GiB) */
+  int solve_path;           /* enum sglm_solve_path of the last solve, -1 before any */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
@@ -201,6 +231,11 @@ int sglm_get_data(sglm_engine *h, double *X, double *y, double *m, double *offse
 
 /* ---- communicators (Spark treeReduce replacement) ----------------------------- */
 int sglm_set_comm(sglm_engine *h, sglm_allreduce_fn fn, void *ctx, int on_device);
+/* This handle's rank in the communicator just set by sglm_set_comm (0 <= rank < its rank count;
+ * known without this call for RCCL and sglm_local_allreduce).  With it the per-iteration scalars
+ * (deviance, Pearson, loglik) are summed across ranks in rank order with compensation, so the
+ * convergence test does not depend on the rank count beyond ~1 ulp. */
+int sglm_set_comm_rank(sglm_engine *h, int rank);
 /* Native RCCL communicator over xGMI.  unique_id: 128 bytes from
  * sglm_rccl_unique_id() on rank 0, broadcast by the caller. */
 int sglm_rccl_unique_id(void *out128);

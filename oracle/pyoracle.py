@@ -24,7 +24,7 @@ NS = 8
 
 class _Opts(C.Structure):
     _fields_ = [("family", C.c_int), ("link", C.c_int), ("tol", C.c_double), ("max_iter", C.c_int),
-                ("verbose", C.c_int), ("npart", C.c_int), ("nthreads", C.c_int)]
+                ("verbose", C.c_int), ("npart", C.c_int), ("nthreads", C.c_int), ("plain_sums", C.c_int)]
 
 
 class _Pre(C.Structure):
@@ -102,7 +102,7 @@ def fit_glm(X, y, family="binomial", link="logit", *, m=None, offset=None, prior
     coefs = np.zeros(p)
     se = np.zeros(p)
     trace = np.full(max_trace, np.nan)
-    o = _Opts(FAMILIES[family], LINKS[link], tol, max_iter, int(verbose), npart, nthreads)
+    o = _Opts(FAMILIES[family], LINKS[link], tol, max_iter, int(verbose), npart, nthreads, 0)
     pre = _Pre(_ptr(coefs), _ptr(se), 0, 0, 0, 0, 0, 0, 0, _ptr(trace), max_trace)
     rc = lib().orc_fit_glm(_ptr(X), n, p, n, _ptr(y), _ptr(m), _ptr(offset), _ptr(prior),
                            C.byref(o), C.byref(pre))
@@ -113,12 +113,14 @@ def fit_glm(X, y, family="binomial", link="logit", *, m=None, offset=None, prior
 
 
 def fit_glm_synth(kind, row0, n, p, seed, family="binomial", link="logit", *, tol=1e-6, max_iter=0, npart=1,
-                  nthreads=8, verbose=False, max_trace=256) -> OraclePreGLM:
+                  nthreads=8, verbose=False, max_trace=256, plain_sums=False) -> OraclePreGLM:
     """Streaming fit of rows [row0, row0+n) of the synthetic design (sparkglm_amd.synth), rows
     regenerated chunk by chunk every iteration (orc_fit_glm_synth): full-size parity without
-    holding X in host RAM."""
+    holding X in host RAM.  plain_sums: the reference's summation order for the deviance and the
+    other scalars (per-partition plain running sums, partitions added in order; npart partitions)
+    instead of compensated sums."""
     coefs, se, trace = np.zeros(p), np.zeros(p), np.full(max_trace, np.nan)
-    o = _Opts(FAMILIES[family], LINKS[link], tol, max_iter, int(verbose), npart, nthreads)
+    o = _Opts(FAMILIES[family], LINKS[link], tol, max_iter, int(verbose), npart, nthreads, int(bool(plain_sums)))
     pre = _Pre(_ptr(coefs), _ptr(se), 0, 0, 0, 0, 0, 0, 0, _ptr(trace), max_trace)
     rc = lib().orc_fit_glm_synth(int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1)),
                                  C.byref(o), C.byref(pre))

@@ -738,9 +738,13 @@ static inline void neumaier(double *s, double *c, double x) {
   *s = t;
 }
 
-/* One pass over rows [row0, row0+n) of the generated design (see the section comment). */
+/* One pass over rows [row0, row0+n) of the generated design (see the section comment).
+ * nseg > 0 (plain_sums): nseg contiguous partitions, each one thread's, its scalars a plain
+ * running sum over its rows in row order (reference BLAS's ones-vector dgemm, GLM.scala:168). */
 static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, int link, int mode,
-                        const double *beta, double mu0, int nthreads, seg_acc *seg) {
+                        const double *beta, double mu0, int nthreads, seg_acc *seg, int nseg) {
+  const int plain = nseg > 0;
+  if (!plain) nseg = ORC_NSEG;
   const int64_t p = g->p;
   const int has_op = g->kind == 2;
 #ifdef _OPENMP
@@ -754,7 +758,7 @@ static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, i
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif
-    for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+    for (int sgi = 0; sgi < nseg; ++sgi) {
       seg_acc *a = &seg[sgi];
       memset(a->s, 0, sizeof a->s);
       memset(a->c, 0, sizeof a->c);
@@ -762,12 +766,15 @@ static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, i
         memset(a->G, 0, sizeof(double) * (size_t)(p * p));
         memset(a->xtwz, 0, sizeof(double) * (size_t)p);
       }
-      const int64_t lo = part_lo(n, sgi, ORC_NSEG), hi = part_lo(n, sgi + 1, ORC_NSEG);
+      const int64_t lo = part_lo(n, sgi, nseg), hi = part_lo(n, sgi + 1, nseg);
       for (int64_t c0 = lo; c0 < hi; c0 += ORC_CH) {
         const int64_t nr = (hi - c0) < ORC_CH ? (hi - c0) : ORC_CH;
         gen_rows(g, row0 + c0, nr, X, ORC_CH, y, has_op ? off : NULL, has_op ? pr : NULL);
         if (mode == SP_YSUM) {
-          neumaier(&a->s[ORC_S_DEV], &a->c[ORC_S_DEV], pairwise_sum(y, nr));
+          if (plain)
+            for (int64_t i = 0; i < nr; ++i) a->s[ORC_S_DEV] += y[i];
+          else
+            neumaier(&a->s[ORC_S_DEV], &a->c[ORC_S_DEV], pairwise_sum(y, nr));
           continue;
         }
         for (int64_t i = 0; i < nr; ++i) {
@@ -809,8 +816,13 @@ static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, i
           }
           ti[ORC_S_SUMW * ORC_CH] = pw;
         }
-        for (int k = 0; k < ORC_NS; ++k)
-          if (k != ORC_S_AUX2) neumaier(&a->s[k], &a->c[k], pairwise_sum(t + k * ORC_CH, nr));
+        for (int k = 0; k < ORC_NS; ++k) {
+          if (k == ORC_S_AUX2) continue;
+          if (plain)
+            for (int64_t i = 0; i < nr; ++i) a->s[k] += t[k * ORC_CH + i];
+          else
+            neumaier(&a->s[k], &a->c[k], pairwise_sum(t + k * ORC_CH, nr));
+        }
         gram_rows(X, ORC_CH, p, 0, nr, w, z, a->G, a->xtwz);
       }
     }
@@ -818,15 +830,22 @@ static void stream_pass(const orc_gen *g, int64_t row0, int64_t n, int family, i
   }
 }
 
-static void seg_total(const seg_acc *seg, int64_t p, int with_gram, double *G, double *xtwz, double *s) {
+/* nseg > 0: plain_sums -- the partition totals added plainly in partition order (GLM.scala:407) */
+static void seg_total(const seg_acc *seg, int64_t p, int with_gram, double *G, double *xtwz, double *s, int nseg) {
   double cs[ORC_NS] = {0};
+  const int plain = nseg > 0;
+  if (!plain) nseg = ORC_NSEG;
   memset(s, 0, sizeof(double) * ORC_NS);
   if (with_gram) {
     memset(G, 0, sizeof(double) * (size_t)(p * p));
     memset(xtwz, 0, sizeof(double) * (size_t)p);
   }
-  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+  for (int sgi = 0; sgi < nseg; ++sgi) {
     for (int k = 0; k < ORC_NS; ++k) {
+      if (plain) {
+        s[k] += seg[sgi].s[k];
+        continue;
+      }
       neumaier(&s[k], &cs[k], seg[sgi].s[k]);
       neumaier(&s[k], &cs[k], seg[sgi].c[k]);
     }
@@ -844,8 +863,9 @@ int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t see
   if (kind < 0 || kind > 3 || n <= 0 || p <= 0) return ORC_EINVAL;
   orc_gen g;
   gen_init(&g, kind, p, seed);
-  seg_acc *seg = (seg_acc *)calloc(ORC_NSEG, sizeof(seg_acc));
-  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+  const int nseg = o->plain_sums ? (o->npart > 0 ? o->npart : 1) : 0, nalloc = nseg > ORC_NSEG ? nseg : ORC_NSEG;
+  seg_acc *seg = (seg_acc *)calloc((size_t)nalloc, sizeof(seg_acc));
+  for (int sgi = 0; sgi < nalloc; ++sgi) {
     seg[sgi].G = (double *)calloc((size_t)(p * p), sizeof(double));
     seg[sgi].xtwz = (double *)calloc((size_t)p, sizeof(double));
   }
@@ -855,12 +875,12 @@ int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t see
   const double fac = family_dev_factor(o->family);
   int rc = ORC_OK;
 
-  stream_pass(&g, row0, n, o->family, o->link, SP_YSUM, NULL, 0.0, o->nthreads, seg);
-  seg_total(seg, p, 0, NULL, NULL, s);
+  stream_pass(&g, row0, n, o->family, o->link, SP_YSUM, NULL, 0.0, o->nthreads, seg, nseg);
+  seg_total(seg, p, 0, NULL, NULL, s, nseg);
   const double ymean = s[ORC_S_DEV] / (double)n; /* GLM.scala:263 / 423 */
   const int init = o->npart > 1 ? ORC_MODE_INIT_MULTI : ORC_MODE_INIT_SINGLE;
-  stream_pass(&g, row0, n, o->family, o->link, init, NULL, ymean, o->nthreads, seg);
-  seg_total(seg, p, 1, Gm, xtwz, s);
+  stream_pass(&g, row0, n, o->family, o->link, init, NULL, ymean, o->nthreads, seg, nseg);
+  seg_total(seg, p, 1, Gm, xtwz, s, nseg);
   double dev = fac * s[ORC_S_DEV], null_dev = dev, dev_old, deltad = 1.0;
   int iter = 0;
   if (out->dev_trace && out->max_trace > 0) out->dev_trace[0] = dev;
@@ -868,8 +888,8 @@ int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t see
     if (o->max_iter > 0 && iter >= o->max_iter) break;
     rc = wls_solve(Gm, xtwz, p, coefs, diag_design); /* wlsSingle (utils.scala:98-107) */
     if (rc) goto done;
-    stream_pass(&g, row0, n, o->family, o->link, ORC_MODE_IRLS, coefs, ymean, o->nthreads, seg);
-    seg_total(seg, p, 1, Gm, xtwz, s);
+    stream_pass(&g, row0, n, o->family, o->link, ORC_MODE_IRLS, coefs, ymean, o->nthreads, seg, nseg);
+    seg_total(seg, p, 1, Gm, xtwz, s, nseg);
     dev_old = dev;
     dev = fac * s[ORC_S_DEV];
     deltad = dev - dev_old;
@@ -897,7 +917,7 @@ int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t see
     out->npart = o->npart > 0 ? o->npart : 1;
   }
 done:
-  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) { free(seg[sgi].G); free(seg[sgi].xtwz); }
+  for (int sgi = 0; sgi < nalloc; ++sgi) { free(seg[sgi].G); free(seg[sgi].xtwz); }
   free(seg); free(Gm); free(xtwz); free(coefs); free(diag_design); free(g.bs);
   return rc;
 }

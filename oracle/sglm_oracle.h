@@ -34,6 +34,11 @@ typedef struct {
   int verbose;     /* GLM.scala:304 */
   int npart;       /* 1 -> fitSingleBinomial semantics; G>1 -> fitMultipleBinomial over G row partitions */
   int nthreads;    /* threads for the partitioned Gram (Spark local[N] analogue) */
+  int plain_sums;  /* orc_fit_glm_synth only: 1 = the reference's summation order for the scalars --
+                      per partition (npart contiguous slices) a plain running sum over its rows, as
+                      the ones-vector dgemm of createBinomialDeviance (GLM.scala:168) computes it in
+                      reference BLAS, then the partition totals summed plainly in partition order
+                      (GLM.scala:404-407); 0 = compensated (Neumaier) sums (the default) */
 } orc_opts;
 
 typedef struct {

@@ -31,7 +31,7 @@ EXPORTS = [
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
     "sglm_pval_normal", "sglm_pval_t", "sglm_create_multi", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
     "sglm_predict_glm", "sglm_predict_new", "sglm_local_comm_create", "sglm_local_comm_destroy",
-    "sglm_local_comm_rank", "sglm_local_allreduce",
+    "sglm_local_comm_rank", "sglm_local_allreduce", "sglm_set_comm_rank",
 ]
 PREDICT_LINK, PREDICT_RESPONSE = 0, 1
 
@@ -61,7 +61,13 @@ class Stats(C.Structure):
                 ("path", C.c_int), ("wide_panels", C.c_int), ("row_kernel_ms", C.c_double),
                 ("gram_kernel_ms", C.c_double), ("load_ms", C.c_double), ("load_bytes", C.c_int64),
                 ("ndev", C.c_int), ("rccl_group", C.c_int), ("dev_passes", C.c_int64),
-                ("overlap_chunks", C.c_int)]
+                ("overlap_chunks", C.c_int), ("comm_path", C.c_int), ("rank_blocks", C.c_int),
+                ("pass_kernel_ms_min", C.c_double), ("proc_chunks", C.c_int), ("proc_chunk_rows", C.c_int64),
+                ("solve_path", C.c_int)]
+
+
+COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}
+SOLVE_PATHS = {-1: "none", 0: "host-cholesky", 1: "host-lu", 2: "device-cholesky", 3: "device-lu"}
 
 
 class GlmDerived(C.Structure):
@@ -119,6 +125,7 @@ def load():
         "sglm_synth_procedural": ([h, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64], C.c_int),
         "sglm_get_data": ([h, dp, dp, dp, dp, dp], C.c_int),
         "sglm_set_comm": ([h, ALLREDUCE_FN, C.c_void_p, C.c_int], C.c_int),
+        "sglm_set_comm_rank": ([h, C.c_int], C.c_int),
         "sglm_rccl_unique_id": ([C.c_void_p], C.c_int),
         "sglm_set_comm_rccl": ([h, C.c_int, C.c_int, C.c_void_p], C.c_int),
         "sglm_fit_glm": ([h, C.POINTER(GlmOpts), C.POINTER(PreGLM)], C.c_int),

@@ -67,6 +67,9 @@ int HostSolver::inverse(double* Ainv) {
   impl_->s.inverse(Ainv);
   return SGLM_OK;
 }
+int HostSolver::path() const {
+  return !impl_->s.has_factor() ? -1 : impl_->s.used_lu() ? SGLM_SOLVE_HOST_LU : SGLM_SOLVE_HOST_CHOL;
+}
 
 static double now_ms() {
   using namespace std::chrono;
@@ -121,6 +124,7 @@ int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out) {
     const double t0 = now_ms();
     const int srv = solver->solve(packed.data(), beta.data());
     be.solve_ms += now_ms() - t0;
+    be.solve_path = solver->path();
     if (srv) {
       if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
       return srv;
@@ -203,6 +207,7 @@ int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, d
     const double t0 = now_ms();
     const int srv = solver->solve(packed.data(), beta);
     be.solve_ms += now_ms() - t0;
+    be.solve_path = solver->path();
     if (srv) {
       if (srv == SGLM_ESINGULAR) set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
       return srv;
@@ -230,6 +235,7 @@ int lm_drive(Backend& be, sglm_prelm* out) {
   rc = solver->inverse(xtxi.data());
   if (rc) return rc;
   be.solve_ms += now_ms() - t0;
+  be.solve_path = solver->path();
   const double ymean = ysum / nrow;  // LM.scala:167-168
   rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
   if (rc) return rc;

@@ -23,6 +23,8 @@ class SolverIface {
   virtual int solve(const double* packed, double* x) = 0;
   virtual int inv_diag(double* d) = 0;
   virtual int inverse(double* Ainv) = 0;
+  // enum sglm_solve_path of the last solve (-1 before any)
+  virtual int path() const = 0;
 };
 
 // Host Cholesky with the LU fallback (solve.cpp).
@@ -33,6 +35,7 @@ class HostSolver : public SolverIface {
   int solve(const double* packed, double* x) override;
   int inv_diag(double* d) override;
   int inverse(double* Ainv) override;
+  int path() const override;
 
  private:
   int64_t p_;
@@ -68,6 +71,7 @@ class Backend {
   virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats
   double solve_ms = 0.0;
+  int solve_path = -1;  // enum sglm_solve_path of the last solve
 };
 
 int glm_drive(Backend& be, const sglm_glm_opts& o, sglm_preglm* out);

@@ -73,8 +73,26 @@ struct Comm {
   int on_device = 0;
   ncclComm_t nccl = nullptr;
   int nranks = 1;
+  int rank = -1;  // this handle's rank (RCCL, the in-process communicator, sglm_set_comm_rank); -1 unknown
   double ms = 0.0;
 };
+
+// Cross-rank sums of the NS scalars (deviance, Pearson, loglik ingredients, ...) in rank order
+// with compensation.  The all-reduce buffer carries, after the packed result, one block of
+// `count` slots per rank in which only the owner's block is non-zero, so the all-reduce -- in
+// whatever order RCCL or the caller adds -- delivers every rank's scalars exactly (x + 0 = x),
+// and each rank then sums them itself, in rank order, Neumaier-compensated: the fit's deviance
+// trajectory no longer depends on how many ranks the rows are spread over beyond ~1 ulp.  A plain
+// all-reduce of the deviance adds up to G - 1 uncompensated roundings of up to half an ulp each
+// (2.4e-7 at 1e9 rows, beside GLM.scala:452's absolute tol 1e-6).  The partition-order sum of the
+// reference (GLM.scala:404-407) is the order used here; only the rounding is compensated.
+void compensated_rank_sum(const double* blocks, int nranks, int64_t count, double* out) {
+  for (int64_t k = 0; k < count; ++k) {
+    double s = 0.0, c = 0.0;
+    for (int r = 0; r < nranks; ++r) neumaier_add(s, c, blocks[(int64_t)r * count + k]);
+    out[k] = s + c;
+  }
+}
 
 // Copy a column-major host block (rows x cols, leading dimension sld) into a packed buffer,
 // on several threads for large blocks (the pageable -> pinned leg of the ingest path).
@@ -103,10 +121,40 @@ void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_
 
 }  // namespace
 
+// ---- in-process communicator: N host threads, one handle each (a JVM driver's thread pool) ----
+// Every rank's call blocks until all N have arrived; the last to arrive sums the N buffers in
+// rank order (deterministic, independent of arrival order) and writes the sum into all of them.
+struct sglm_local_comm {
+  int nranks = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<double*> bufs;
+  int64_t count = -1;
+  bool failed = false;  // this round: a rank passed another count
+  bool result = false;  // the last completed round failed (read by its waiters only)
+  struct Rank {
+    sglm_local_comm* c;
+    int rank;
+  };
+  std::vector<Rank> ranks;
+};
+
+namespace {
+// The rank a caller-supplied communicator context stands for, when the engine can tell: the
+// in-process communicator's rank contexts (sglm_local_comm_rank); -1 otherwise.
+int known_rank(sglm_allreduce_fn fn, void* ctx) {
+  if (fn == &sglm_local_allreduce && ctx) return static_cast<sglm_local_comm::Rank*>(ctx)->rank;
+  return -1;
+}
+}  // namespace
+
 struct sglm_engine : public Backend {
   int device = 0;
   hipStream_t st = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t evc = nullptr;  // end of the pass's device all-reduce (comm time = ev2 -> evc)
   int ncu = 256;
   // resident shard
   int64_t n = 0, p = 0, n_pad = 0, nblocks = 0;
@@ -166,6 +214,10 @@ struct sglm_engine : public Backend {
   bool has_sched[2] = {false, false};
   hipEvent_t evm = nullptr;
   rocblas_handle blas = nullptr;
+  // wide-path device solve (SGLM_WIDE_SOLVE): 1 LU + explicit inverse (Breeze inv: dgetrf + dgetri,
+  // utils.scala:103-105), 0 Cholesky (potrf / potrs / potri)
+  int wide_lu = 1;
+  int64_t proc_scratch_max = 0;  // SGLM_PROC_SCRATCH_MAX (GiB): cap on the procedural chunk scratch (0: none)
   // stats
   int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
@@ -175,7 +227,8 @@ struct sglm_engine : public Backend {
   double* hstage[2] = {nullptr, nullptr};
   hipEvent_t evstage[2] = {nullptr, nullptr};
   int stage_k = 0;
-  int64_t rows_loaded = 0;  // rows written since the shard was reserved
+  int64_t rows_loaded = 0;  // rows covered by the blocks written since the shard was reserved
+  std::vector<std::pair<int64_t, int64_t>> written;  // those blocks' row ranges, disjoint, sorted
   double load_ms = 0.0;     // host wall time in set_data / set_rows (staging + H2D)
   int64_t load_bytes = 0;
   // new-row scoring (sglm_predict_new): a device scratch, separate from the resident shard
@@ -204,6 +257,7 @@ struct sglm_engine : public Backend {
     }
     n = p = n_pad = nblocks = 0;
     rows_loaded = 0;
+    written.clear();
     procx = ProcX{};
     for (double** ptr : {&dxsc, &dchunks}) {
       if (*ptr) (void)hipFree(*ptr);
@@ -223,6 +277,7 @@ struct sglm_engine : public Backend {
       *ptr = nullptr;
     }
     xs_cap = vs_cap = 0;
+    dsmall_cap = 0;
     for (int k = 0; k < 2; ++k) {
       if (hstage[k]) (void)hipHostFree(hstage[k]);
       if (evstage[k]) (void)hipEventDestroy(evstage[k]);
@@ -250,8 +305,9 @@ struct sglm_engine : public Backend {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
+    if (evc) (void)hipEventDestroy(evc);
     if (st) (void)hipStreamDestroy(st);
-    ev0 = ev1 = ev2 = nullptr;
+    ev0 = ev1 = ev2 = evc = nullptr;
     st = nullptr;
   }
 
@@ -260,7 +316,10 @@ struct sglm_engine : public Backend {
   int npart() const override { return group() ? (int)subs.size() : comm.nranks; }
 
   // ---- communicator helpers ----
-  int allreduce_device(double* dbuf, int64_t count) {
+  // after_pass: dbuf is the pass just enqueued (ev2 marks its end on st); the RCCL time is then
+  // ev2 -> evc on the device (this rank's wait for the others included), not the host wall time
+  // of a synchronize that would also cover the pass kernels.
+  int allreduce_device(double* dbuf, int64_t count, bool after_pass = false) {
     if (comm.kind == 2) {
       const double t0 = now_ms();
       ncclResult_t r = ncclAllReduce(dbuf, dbuf, (size_t)count, ncclFloat64, ncclSum, comm.nccl, st);
@@ -268,8 +327,15 @@ struct sglm_engine : public Backend {
         set_error(std::string("RCCL ncclAllReduce: ") + ncclGetErrorString(r));
         return SGLM_ECOMM;
       }
+      if (after_pass) HIPCHK(hipEventRecord(evc, st));
       HIPCHK(hipStreamSynchronize(st));
-      comm.ms += now_ms() - t0;
+      if (after_pass) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ev2, evc));
+        comm.ms += ms;
+      } else {
+        comm.ms += now_ms() - t0;
+      }
     } else if (comm.kind == 1 && comm.on_device) {
       HIPCHK(hipStreamSynchronize(st));
       const double t0 = now_ms();
@@ -293,17 +359,66 @@ struct sglm_engine : public Backend {
     return SGLM_OK;
   }
   bool comm_on_device() const { return comm.kind == 2 || (comm.kind == 1 && comm.on_device); }
-  // all-reduce a small host vector through whichever path the communicator uses
+  // scalars summed across ranks through rank blocks (compensated_rank_sum): needs >1 rank and a
+  // known own rank; otherwise the communicator's plain sum
+  bool gather_ranks() const { return comm.kind != 0 && comm.nranks > 1 && comm.rank >= 0 && comm.rank < comm.nranks; }
+  int64_t dsmall_cap = 0;
+  int ensure_small(int64_t count) {
+    if (count <= dsmall_cap && dsmall) return SGLM_OK;
+    if (dsmall) HIPCHK(hipFree(dsmall));
+    dsmall = nullptr;
+    dsmall_cap = std::max<int64_t>(64, count);
+    HIPCHK(hipMalloc(&dsmall, sizeof(double) * dsmall_cap));
+    return SGLM_OK;
+  }
+  // all-reduce a small host vector (count scalar sums) through whichever path the communicator uses
   int allreduce_small(double* h, int64_t count) {
-    if (comm_on_device()) {
-      HIPCHK(hipMemcpyAsync(dsmall, h, sizeof(double) * count, hipMemcpyHostToDevice, st));
-      int rc = allreduce_device(dsmall, count);
-      if (rc) return rc;
-      HIPCHK(hipMemcpyAsync(h, dsmall, sizeof(double) * count, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      return SGLM_OK;
+    if (comm.kind == 0) return SGLM_OK;
+    std::vector<double> blocks;
+    double* b = h;
+    int64_t len = count;
+    if (gather_ranks()) {  // this rank's values in its own block, zeros elsewhere
+      blocks.assign((size_t)(count * comm.nranks), 0.0);
+      std::memcpy(blocks.data() + (int64_t)comm.rank * count, h, sizeof(double) * count);
+      b = blocks.data();
+      len = count * comm.nranks;
     }
-    return allreduce_host(h, count);
+    if (comm_on_device()) {
+      if (int rc = ensure_small(len)) return rc;
+      HIPCHK(hipMemcpyAsync(dsmall, b, sizeof(double) * len, hipMemcpyHostToDevice, st));
+      int rc = allreduce_device(dsmall, len);
+      if (rc) return rc;
+      HIPCHK(hipMemcpyAsync(b, dsmall, sizeof(double) * len, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    } else if (int rc = allreduce_host(b, len)) {
+      return rc;
+    }
+    if (b != h) compensated_rank_sum(b, comm.nranks, count, h);
+    return SGLM_OK;
+  }
+  // dred / hred hold at least len doubles (the packed result + the rank blocks of its scalars)
+  int ensure_red_len(int64_t len) {
+    if (len <= red_cap && dred) return SGLM_OK;
+    if (dred) HIPCHK(hipFree(dred));
+    if (hred) HIPCHK(hipHostFree(hred));
+    dred = hred = nullptr;
+    HIPCHK(hipMalloc(&dred, sizeof(double) * len));
+    HIPCHK(hipHostMalloc(&hred, sizeof(double) * len, hipHostMallocDefault));
+    if (dbeta) HIPCHK(hipFree(dbeta));
+    if (hbeta) HIPCHK(hipHostFree(hbeta));
+    dbeta = hbeta = nullptr;
+    HIPCHK(hipMalloc(&dbeta, sizeof(double) * len));
+    HIPCHK(hipHostMalloc(&hbeta, sizeof(double) * len, hipHostMallocDefault));
+    red_cap = len;
+    return SGLM_OK;
+  }
+  // this shard's scalars into rank block `r` of the nr blocks after the packed result, zeros in the
+  // others (device buffer, on st)
+  int stage_rank_block(int r, int nr) {
+    const int64_t plen = packed_len(p), sc = tri_count(p) + p;
+    HIPCHK(hipMemsetAsync(dred + plen, 0, sizeof(double) * (size_t)(NS * nr), st));
+    HIPCHK(hipMemcpyAsync(dred + plen + (int64_t)r * NS, dred + sc, sizeof(double) * NS, hipMemcpyDeviceToDevice, st));
+    return SGLM_OK;
   }
 
   void free_schedule() {
@@ -486,7 +601,9 @@ struct sglm_engine : public Backend {
     HIPCHK(hipMemGetInfo(&fr, &tot));
     const int64_t ncols8 = (p + 7) / 8 * 8;
     const size_t margin = (size_t)4 << 30;
-    const int64_t cap_rows = fr > margin ? (int64_t)((fr - margin) / (sizeof(double) * (size_t)ncols8)) : 0;
+    size_t room = fr > margin ? fr - margin : 0;
+    if (proc_scratch_max > 0) room = std::min(room, (size_t)proc_scratch_max << 30);
+    const int64_t cap_rows = (int64_t)(room / (sizeof(double) * (size_t)ncols8));
     int64_t c = std::min<int64_t>(n_pad, cap_rows / 32 * 32);
     if (c < std::min<int64_t>(n_pad, (int64_t)1 << 20)) return SGLM_OK;  // too little room: in-kernel generation
     int64_t k = (n_pad + c - 1) / c;
@@ -566,8 +683,7 @@ struct sglm_engine : public Backend {
       HIPCHK(hipHostMalloc(&hbeta, sizeof(double) * need_red, hipHostMallocDefault));
       red_cap = need_red;
     }
-    if (!dsmall) HIPCHK(hipMalloc(&dsmall, sizeof(double) * 64));
-    return SGLM_OK;
+    return ensure_small(64);
   }
 
   int alloc_data(int64_t n_, int64_t p_, bool has_m, bool has_off, bool has_prior, bool proc = false) {
@@ -666,6 +782,14 @@ struct sglm_engine : public Backend {
       return SGLM_EINVAL;
     }
     if (nr == 0) return SGLM_OK;
+    // blocks must not overlap (sglm.h): a repeated or overlapping block would count its rows twice
+    // and let a fit run over reserved rows that were never written (zero X, y)
+    auto it = std::lower_bound(written.begin(), written.end(), std::make_pair(row0, row0));
+    if ((it != written.end() && it->first < row0 + nr) || (it != written.begin() && std::prev(it)->second > row0)) {
+      set_error("requirement failed: rows [" + std::to_string(row0) + ", " + std::to_string(row0 + nr) +
+                ") overlap a block already written (sglm_set_rows blocks must not overlap)");
+      return SGLM_EINVAL;
+    }
     const double t0 = now_ms();
     int rc = h2d_block(dX + row0, n_pad, X, ldx, nr, p);
     for (auto pr : {std::make_pair(dy, yv), std::make_pair(dm, mv), std::make_pair(doff, ov),
@@ -676,6 +800,16 @@ struct sglm_engine : public Backend {
     load_ms += now_ms() - t0;
     const int nvec = 1 + (mv != nullptr) + (ov != nullptr) + (pv != nullptr);
     load_bytes += (int64_t)sizeof(double) * nr * (p + nvec);
+    it = written.insert(std::lower_bound(written.begin(), written.end(), std::make_pair(row0, row0)),
+                        std::make_pair(row0, row0 + nr));
+    if (std::next(it) != written.end() && std::next(it)->first == it->second) {  // merge touching neighbours
+      it->second = std::next(it)->second;
+      written.erase(std::next(it));
+    }
+    if (it != written.begin() && std::prev(it)->second == it->first) {
+      std::prev(it)->second = it->second;
+      written.erase(it);
+    }
     rows_loaded += nr;
     return SGLM_OK;
   }
@@ -748,14 +882,11 @@ struct sglm_engine : public Backend {
 
   // ---- Backend ----
   int global_sums(double* out2) override {
-    if (group()) {  // shard order, as createBinomialDeviance sums partitions (GLM.scala:407)
-      out2[0] = out2[1] = 0.0;
-      for (sglm_engine* s : subs) {
-        double t[2];
-        if (int rc = s->global_sums(t)) return rc;
-        out2[0] += t[0];
-        out2[1] += t[1];
-      }
+    if (group()) {  // shard order, as the reference sums partitions (GLM.scala:420-423), compensated
+      std::vector<double> blocks(2 * subs.size());
+      for (size_t d = 0; d < subs.size(); ++d)
+        if (int rc = subs[d]->global_sums(blocks.data() + 2 * d)) return rc;
+      compensated_rank_sum(blocks.data(), (int)subs.size(), 2, out2);
       return SGLM_OK;
     }
     HIPCHK(hipSetDevice(device));
@@ -785,22 +916,31 @@ struct sglm_engine : public Backend {
 
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
     if (group()) return group_pass(mode, beta, mu0, ybar, family, link, packed);
+    const int64_t plen = packed_len(p), sc = tri_count(p) + p;
+    const int R = gather_ranks() ? comm.nranks : 0;  // rank blocks of the scalars (compensated_rank_sum)
+    const int64_t len = plen + (int64_t)NS * R;
+    if (int rc = ensure_red_len(len)) return rc;
     int rc = enqueue_pass(mode, beta, mu0, ybar, family, link);
     if (rc) return rc;
-    const int64_t plen = packed_len(p);
     if (comm_on_device()) {
-      rc = allreduce_device(dred, plen);
+      if (R && (rc = stage_rank_block(comm.rank, R))) return rc;
+      rc = allreduce_device(dred, len, true);
       if (rc) return rc;
     }
-    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * plen, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * (comm_on_device() ? len : plen), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     rc = pass_timing();
     if (rc) return rc;
     red_on_device = comm_on_device() || comm.kind == 0;
     if (!comm_on_device()) {
-      rc = allreduce_host(hred, plen);
+      if (R) {
+        std::fill(hred + plen, hred + len, 0.0);
+        std::memcpy(hred + plen + (int64_t)comm.rank * NS, hred + sc, sizeof(double) * NS);
+      }
+      rc = allreduce_host(hred, comm.kind == 0 ? plen : len);
       if (rc) return rc;
     }
+    if (R) compensated_rank_sum(hred + plen, R, NS, hred + sc);
     std::memcpy(packed, hred, sizeof(double) * plen);
     return SGLM_OK;
   }
@@ -1018,28 +1158,50 @@ struct sglm_engine : public Backend {
   // Distinct devices: ncclAllReduce of the packed buffers in one RCCL group call (xGMI), every
   // shard ends with the sum.  Repeated devices (rehearsal on fewer GPUs): host sums in shard
   // order.  Either way the wide-path device solver reads shard 0's buffers.
+  // The scalars are summed in shard order with compensation either way (compensated_rank_sum).
+  // comm_ms: RCCL -- the shortest span from a shard's pass end (ev2) to its all-reduce end (evc),
+  // i.e. the collective after the last shard arrived; host sums -- the host time of the sum.
   int group_pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) {
-    const int64_t plen = packed_len(subs[0]->p);
+    const int64_t pp = subs[0]->p, plen = packed_len(pp), sc = tri_count(pp) + pp;
+    const int D = (int)subs.size();
+    const int64_t len = plen + (int64_t)NS * D;
+    for (sglm_engine* s : subs) {
+      HIPCHK(hipSetDevice(s->device));
+      if (int rc = s->ensure_red_len(len)) return rc;
+    }
     for (sglm_engine* s : subs)
       if (int rc = s->enqueue_pass(mode, beta, mu0, ybar, family, link)) return rc;
-    const double t0 = now_ms();
     if (!gcomms.empty()) {
+      for (int d = 0; d < D; ++d) {
+        HIPCHK(hipSetDevice(subs[d]->device));
+        if (int rc = subs[d]->stage_rank_block(d, D)) return rc;
+      }
       ncclResult_t r = ncclGroupStart();
-      for (size_t d = 0; d < subs.size() && r == ncclSuccess; ++d)
-        r = ncclAllReduce(subs[d]->dred, subs[d]->dred, (size_t)plen, ncclFloat64, ncclSum, gcomms[d], subs[d]->st);
+      for (int d = 0; d < D && r == ncclSuccess; ++d)
+        r = ncclAllReduce(subs[d]->dred, subs[d]->dred, (size_t)len, ncclFloat64, ncclSum, gcomms[d], subs[d]->st);
       ncclResult_t r2 = ncclGroupEnd();
       if (r != ncclSuccess || r2 != ncclSuccess) {
         set_error(std::string("RCCL ncclAllReduce (group): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
         return SGLM_ECOMM;
       }
+      for (sglm_engine* s : subs) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipEventRecord(s->evc, s->st));
+      }
       sglm_engine* s0 = subs[0];
       HIPCHK(hipSetDevice(s0->device));
-      HIPCHK(hipMemcpyAsync(s0->hred, s0->dred, sizeof(double) * plen, hipMemcpyDeviceToHost, s0->st));
+      HIPCHK(hipMemcpyAsync(s0->hred, s0->dred, sizeof(double) * len, hipMemcpyDeviceToHost, s0->st));
+      double cms = -1.0;
       for (sglm_engine* s : subs) {
         HIPCHK(hipSetDevice(s->device));
         HIPCHK(hipStreamSynchronize(s->st));
         if (int rc = s->pass_timing()) return rc;
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, s->ev2, s->evc));
+        cms = cms < 0.0 ? ms : std::min(cms, (double)ms);
       }
+      comm.ms += std::max(cms, 0.0);
+      compensated_rank_sum(s0->hred + plen, D, NS, s0->hred + sc);
       std::memcpy(packed, s0->hred, sizeof(double) * plen);
       s0->red_on_device = true;
     } else {
@@ -1052,12 +1214,16 @@ struct sglm_engine : public Backend {
         HIPCHK(hipStreamSynchronize(s->st));
         if (int rc = s->pass_timing()) return rc;
       }
-      std::memcpy(packed, subs[0]->hred, sizeof(double) * plen);
-      for (size_t d = 1; d < subs.size(); ++d)
-        for (int64_t k = 0; k < plen; ++k) packed[k] += subs[d]->hred[k];
+      const double t0 = now_ms();
+      std::memcpy(packed, subs[0]->hred, sizeof(double) * sc);
+      for (int d = 1; d < D; ++d)
+        for (int64_t k = 0; k < sc; ++k) packed[k] += subs[(size_t)d]->hred[k];
+      std::vector<double> blocks((size_t)(NS * D));
+      for (int d = 0; d < D; ++d) std::memcpy(blocks.data() + (int64_t)d * NS, subs[(size_t)d]->hred + sc, sizeof(double) * NS);
+      compensated_rank_sum(blocks.data(), D, NS, packed + sc);
       subs[0]->red_on_device = false;
+      comm.ms += now_ms() - t0;
     }
-    comm.ms += now_ms() - t0;
     return SGLM_OK;
   }
 
@@ -1078,13 +1244,11 @@ struct sglm_engine : public Backend {
   }
 
   int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) override {
-    if (group()) {
-      for (int k = 0; k < NS; ++k) s[k] = 0.0;
-      for (sglm_engine* sub : subs) {
-        double t[NS];
-        if (int rc = sub->stats(mode, beta, mu0, ybar, family, link, t)) return rc;
-        for (int k = 0; k < NS; ++k) s[k] += t[k];
-      }
+    if (group()) {  // shard order, compensated (compensated_rank_sum)
+      std::vector<double> blocks((size_t)NS * subs.size());
+      for (size_t d = 0; d < subs.size(); ++d)
+        if (int rc = subs[d]->stats(mode, beta, mu0, ybar, family, link, blocks.data() + NS * d)) return rc;
+      compensated_rank_sum(blocks.data(), (int)subs.size(), NS, s);
       return SGLM_OK;
     }
     HIPCHK(hipSetDevice(device));
@@ -1128,33 +1292,47 @@ struct sglm_engine : public Backend {
 };
 
 // =====================================================================================
-// Device solver for wide p: Cholesky on the GPU from the reduced buffer.
-// A matrix potrf rejects (not positive definite) is handed to the host solver, whose LU
-// fallback keeps Breeze inv()'s semantics, exactly as on the narrow path.
+// Device solver for wide p, from the reduced buffer on the GPU.
+// Default: the reference's own algorithm -- LU with partial pivoting and the explicit inverse
+// (Breeze inv = LAPACK dgetrf + dgetri, utils.scala:103-105, 134-136) by rocSOLVER, then
+// coefs = inv * X'Wz summed in the reference's order (inv_gemv_kernel) and stdErr from diag(inv).
+// SGLM_WIDE_SOLVE=chol: Cholesky (potrf / potrs, potri for the standard errors), switching to the
+// LU route when potrf rejects the matrix or its pivots flag it ill-conditioned (solve.hpp).
+// Exact singularity (a zero pivot of dgetrf) -> MatrixSingularException, as Breeze's inv.
+// Either algorithm is within the reference's own spread: on the same X'WX, LAPACK's blocked
+// dgetrf/dgetri and an unblocked restatement part by ~cond * eps (oracle/lu_floor.py).
 // =====================================================================================
 namespace {
 
 struct DeviceSolver : public SolverIface {
   sglm_engine* e;
   int64_t p;
-  double *dA = nullptr, *dB = nullptr, *dAi = nullptr, *dpk = nullptr;
-  rocblas_int* dinfo = nullptr;
-  std::unique_ptr<HostSolver> host;
+  double *dA = nullptr, *dB = nullptr, *dAi = nullptr, *dpk = nullptr, *dx = nullptr;
+  rocblas_int *dinfo = nullptr, *dipiv = nullptr;
   std::vector<double> ldiag;
-  bool on_host = false, have_factor = false;
+  int kind = 0;  // 0 none, 1 Cholesky factor in dA, 2 explicit inverse in dA (LU route)
   DeviceSolver(sglm_engine* eng, int64_t pp) : e(eng), p(pp) {}
+  int path() const override { return kind == 1 ? SGLM_SOLVE_DEVICE_CHOL : kind == 2 ? SGLM_SOLVE_DEVICE_LU : -1; }
   ~DeviceSolver() override {
     (void)hipSetDevice(e->device);
-    for (double* ptr : {dA, dB, dAi, dpk})
+    for (double* ptr : {dA, dB, dAi, dpk, dx})
       if (ptr) (void)hipFree(ptr);
     if (dinfo) (void)hipFree(dinfo);
+    if (dipiv) (void)hipFree(dipiv);
   }
   int alloc() {
     if (dA) return SGLM_OK;
     HIPCHK(hipMalloc(&dA, sizeof(double) * (size_t)(p * p)));
     HIPCHK(hipMalloc(&dAi, sizeof(double) * (size_t)(p * p)));
     HIPCHK(hipMalloc(&dB, sizeof(double) * (size_t)p));
+    HIPCHK(hipMalloc(&dx, sizeof(double) * (size_t)p));
     HIPCHK(hipMalloc(&dinfo, sizeof(rocblas_int)));
+    HIPCHK(hipMalloc(&dipiv, sizeof(rocblas_int) * (size_t)p));
+    return SGLM_OK;
+  }
+  int read_info(rocblas_int* info) {
+    HIPCHK(hipMemcpyAsync(info, dinfo, sizeof *info, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
     return SGLM_OK;
   }
   int solve(const double* packed, double* x) override {
@@ -1168,6 +1346,8 @@ struct DeviceSolver : public SolverIface {
       HIPCHK(hipMemcpyAsync(dpk, packed, sizeof(double) * (size_t)packed_len(p), hipMemcpyHostToDevice, e->st));
       src = dpk;
     }
+    kind = 0;
+    if (e->wide_lu) return solve_lu(src, x);
     HIPCHK(launch_unpack_lower(src, (int)p, dA, dB, e->st));
     if (rocsolver_dpotrf(e->blas, rocblas_fill_lower, (rocblas_int)p, dA, (rocblas_int)p, dinfo) !=
         rocblas_status_success) {
@@ -1188,14 +1368,9 @@ struct DeviceSolver : public SolverIface {
         const double a = packed[j * (j + 1) / 2 + j];
         if (a > 0.0) r = std::fmin(r, ldiag[(size_t)j] * ldiag[(size_t)j] / a);
       }
-      if (r < LU_SWITCH_RATIO) info = -1;  // ill-conditioned: the reference's LU inverse on the host
+      if (r < LU_SWITCH_RATIO) info = -1;  // ill-conditioned: the reference's LU inverse
     }
-    if (info != 0) {
-      on_host = true;
-      have_factor = false;
-      if (!host) host = std::make_unique<HostSolver>(p);
-      return host->solve(packed, x);
-    }
+    if (info != 0) return solve_lu(src, x);  // not positive definite / ill-conditioned
     if (rocsolver_dpotrs(e->blas, rocblas_fill_lower, (rocblas_int)p, 1, dA, (rocblas_int)p, dB, (rocblas_int)p) !=
         rocblas_status_success) {
       set_error("rocsolver_dpotrs failed");
@@ -1203,11 +1378,38 @@ struct DeviceSolver : public SolverIface {
     }
     HIPCHK(hipMemcpyAsync(x, dB, sizeof(double) * (size_t)p, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    on_host = false;
-    have_factor = true;
+    kind = 1;
     return SGLM_OK;
   }
-  // inv(A) (lower triangle) into dAi from the kept factor
+  // inv(A) by dgetrf + dgetri in dA, x = inv(A) b (utils.scala:103-104)
+  int solve_lu(const double* src, double* x) {
+    HIPCHK(launch_unpack_lower(src, (int)p, dA, dB, e->st, true));
+    if (rocsolver_dgetrf(e->blas, (rocblas_int)p, (rocblas_int)p, dA, (rocblas_int)p, dipiv, dinfo) !=
+        rocblas_status_success) {
+      set_error("rocsolver_dgetrf failed");
+      return SGLM_EHIP;
+    }
+    rocblas_int info = 0;
+    if (int rc = read_info(&info)) return rc;
+    if (info != 0) {
+      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return SGLM_ESINGULAR;
+    }
+    if (rocsolver_dgetri(e->blas, (rocblas_int)p, dA, (rocblas_int)p, dipiv, dinfo) != rocblas_status_success) {
+      set_error("rocsolver_dgetri failed");
+      return SGLM_EHIP;
+    }
+    HIPCHK(launch_inv_gemv(dA, (int)p, dB, dx, e->st));
+    HIPCHK(hipMemcpyAsync(x, dx, sizeof(double) * (size_t)p, hipMemcpyDeviceToHost, e->st));
+    if (int rc = read_info(&info)) return rc;
+    if (info != 0) {
+      set_error("breeze.linalg.MatrixSingularException: X'WX is singular");
+      return SGLM_ESINGULAR;
+    }
+    kind = 2;
+    return SGLM_OK;
+  }
+  // inv(A) (lower triangle) into dAi from the kept Cholesky factor
   int device_inverse() {
     HIPCHK(hipMemcpyAsync(dAi, dA, sizeof(double) * (size_t)(p * p), hipMemcpyDeviceToDevice, e->st));
     if (rocsolver_dpotri(e->blas, rocblas_fill_lower, (rocblas_int)p, dAi, (rocblas_int)p, dinfo) !=
@@ -1218,29 +1420,28 @@ struct DeviceSolver : public SolverIface {
     return SGLM_OK;
   }
   int inv_diag(double* d) override {
-    if (on_host) return host->inv_diag(d);
-    if (!have_factor) {
+    if (kind == 0) {
       for (int64_t i = 0; i < p; ++i) d[i] = 0.0;
       return SGLM_OK;
     }
     HIPCHK(hipSetDevice(e->device));
-    int rc = device_inverse();
-    if (rc) return rc;
-    HIPCHK(hipMemcpy2DAsync(d, sizeof(double), dAi, sizeof(double) * (size_t)(p + 1), sizeof(double), (size_t)p,
-                            hipMemcpyDeviceToHost, e->st));
+    if (kind == 1)
+      if (int rc = device_inverse()) return rc;
+    HIPCHK(hipMemcpy2DAsync(d, sizeof(double), kind == 1 ? dAi : dA, sizeof(double) * (size_t)(p + 1), sizeof(double),
+                            (size_t)p, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     return SGLM_OK;
   }
   int inverse(double* Ainv) override {
-    if (on_host) return host->inverse(Ainv);
-    if (!have_factor) return SGLM_OK;
+    if (kind == 0) return SGLM_OK;
     HIPCHK(hipSetDevice(e->device));
-    int rc = device_inverse();
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(Ainv, dAi, sizeof(double) * (size_t)(p * p), hipMemcpyDeviceToHost, e->st));
+    if (kind == 1)
+      if (int rc = device_inverse()) return rc;
+    HIPCHK(hipMemcpyAsync(Ainv, kind == 1 ? dAi : dA, sizeof(double) * (size_t)(p * p), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    for (int64_t j = 0; j < p; ++j)
-      for (int64_t i = 0; i < j; ++i) Ainv[i + j * p] = Ainv[j + i * p];
+    if (kind == 1)
+      for (int64_t j = 0; j < p; ++j)
+        for (int64_t i = 0; i < j; ++i) Ainv[i + j * p] = Ainv[j + i * p];
     return SGLM_OK;
   }
 };
@@ -1263,14 +1464,26 @@ struct ExternalBackend : public Backend {
   sglm_allreduce_fn fn;
   void* ctx;
   int nranks = 1;
-  ExternalBackend(const sglm_backend* b, sglm_allreduce_fn f, void* c) : be(b), fn(f), ctx(c) {}
+  int rank = -1;  // known for the in-process communicator: scalars then summed in rank blocks
+  ExternalBackend(const sglm_backend* b, sglm_allreduce_fn f, void* c) : be(b), fn(f), ctx(c), rank(known_rank(f, c)) {}
   int64_t ncols() const override { return be->p; }
   int npart() const override { return nranks; }
-  int reduce(double* buf, int64_t count) {
+  int reduce_raw(double* buf, int64_t count) {
     if (fn && fn(ctx, buf, count, nullptr, 0) != 0) {
       set_error("caller all-reduce failed");
       return SGLM_ECOMM;
     }
+    return SGLM_OK;
+  }
+  // buf[0, count): the last nsc entries are scalar sums -- through rank blocks when the rank is known
+  int reduce(double* buf, int64_t count, int64_t nsc) {
+    if (!(fn && rank >= 0 && rank < nranks && nranks > 1)) return reduce_raw(buf, count);
+    std::vector<double> b((size_t)(count + nsc * nranks), 0.0);
+    std::memcpy(b.data(), buf, sizeof(double) * count);
+    std::memcpy(b.data() + count + (int64_t)rank * nsc, buf + count - nsc, sizeof(double) * nsc);
+    if (int rc = reduce_raw(b.data(), (int64_t)b.size())) return rc;
+    std::memcpy(buf, b.data(), sizeof(double) * (count - nsc));
+    compensated_rank_sum(b.data() + count, nranks, nsc, buf + count - nsc);
     return SGLM_OK;
   }
   int global_sums(double* out2) override {
@@ -1279,10 +1492,10 @@ struct ExternalBackend : public Backend {
       return SGLM_EINVAL;
     }
     double one[1] = {1.0};
-    int rc = reduce(one, 1);  // counts the ranks joined by the communicator
+    int rc = reduce_raw(one, 1);  // counts the ranks joined by the communicator
     if (rc) return rc;
     nranks = (int)std::lround(one[0]);
-    return reduce(out2, 2);
+    return reduce(out2, 2, 2);
   }
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
     (void)family;
@@ -1291,7 +1504,7 @@ struct ExternalBackend : public Backend {
       set_error("external backend pass failed");
       return SGLM_EINVAL;
     }
-    return reduce(packed, packed_len(be->p));
+    return reduce(packed, packed_len(be->p), NS);
   }
   int stats(int mode, const double* beta, double mu0, double ybar, int family, int link, double* s) override {
     std::vector<double> packed((size_t)packed_len(be->p));
@@ -1360,6 +1573,7 @@ int sglm_create(int device, sglm_engine** out) {
   if ((e = hipEventCreate(&h->ev0)) != hipSuccess) return fail(e, "hipEventCreate");
   if ((e = hipEventCreate(&h->ev1)) != hipSuccess) return fail(e, "hipEventCreate");
   if ((e = hipEventCreate(&h->ev2)) != hipSuccess) return fail(e, "hipEventCreate");
+  if ((e = hipEventCreate(&h->evc)) != hipSuccess) return fail(e, "hipEventCreate");
   hipDeviceProp_t prop;
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e, "hipGetDeviceProperties");
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -1377,6 +1591,8 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
+  if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "chol") != 0;
+  if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
   *out = h;
   return SGLM_OK;
 }
@@ -1513,6 +1729,7 @@ int sglm_set_data_device(sglm_engine* h, const double* dX, int64_t n, int64_t p,
   if (dprior) HIPCHK(hipMemcpyAsync(h->dprior, dprior, vb, kind, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   h->rows_loaded = n;
+  h->written.assign(1, std::make_pair((int64_t)0, n));
   return SGLM_OK;
 }
 
@@ -1540,6 +1757,7 @@ static int synth_impl(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t
                       h->dprior, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   h->rows_loaded = n;
+  h->written.assign(1, std::make_pair((int64_t)0, n));
   if (proc) {
     h->procx.on = 1;
     h->procx.kind = kind;
@@ -1611,11 +1829,12 @@ int sglm_set_comm(sglm_engine* h, sglm_allreduce_fn fn, void* ctx, int on_device
   h->comm.ctx = ctx;
   h->comm.on_device = on_device;
   h->comm.nranks = 1;
+  h->comm.rank = known_rank(fn, ctx);
   if (fn) {  // count the ranks joined by the caller's communicator
     double one[1] = {1.0};
     if (on_device) {
       HIPCHK(hipSetDevice(h->device));
-      if (!h->dsmall) HIPCHK(hipMalloc(&h->dsmall, sizeof(double) * 64));
+      if (int rc = h->ensure_small(64)) return rc;
       HIPCHK(hipMemcpy(h->dsmall, one, sizeof(double), hipMemcpyHostToDevice));
       if (fn(ctx, h->dsmall, 1, (void*)h->st, 1) != 0) {
         set_error("caller all-reduce failed");
@@ -1663,7 +1882,19 @@ int sglm_set_comm_rccl(sglm_engine* h, int nranks, int rank, const void* unique_
   }
   h->comm.kind = 2;
   h->comm.nranks = nranks;
-  if (!h->dsmall) HIPCHK(hipMalloc(&h->dsmall, sizeof(double) * 64));
+  h->comm.rank = rank;
+  if (int rc = h->ensure_small(64)) return rc;
+  return SGLM_OK;
+}
+
+int sglm_set_comm_rank(sglm_engine* h, int rank) {
+  if (int rc = check_handle(h)) return rc;
+  if (int rc = no_group(h, "sglm_set_comm_rank")) return rc;
+  if (h->comm.kind == 0 || rank < 0 || rank >= h->comm.nranks) {
+    set_error("requirement failed: a communicator joined first (sglm_set_comm), 0 <= rank < its rank count");
+    return SGLM_EINVAL;
+  }
+  h->comm.rank = rank;
   return SGLM_OK;
 }
 
@@ -1809,12 +2040,18 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
       out->load_ms += s.load_ms;
       out->load_bytes += s.load_bytes;
     }
+    out->pass_kernel_ms_min = out->pass_kernel_ms;
+    for (size_t d = 1; d < h->subs.size(); ++d)
+      out->pass_kernel_ms_min = std::min(out->pass_kernel_ms_min, h->subs[d]->pass_ms);
     out->comm_ms = h->comm.ms;
     out->solve_ms = h->solve_ms;
     out->ndev = (int)h->subs.size();
     out->rccl_group = h->gcomms.empty() ? 0 : 1;
     out->dev_passes = h->dev_passes;
     out->overlap_chunks = h->subs.empty() ? 0 : h->subs[0]->ov_chunks();
+    out->comm_path = h->gcomms.empty() ? SGLM_COMM_GROUP_HOST : SGLM_COMM_GROUP_RCCL;
+    out->rank_blocks = 1;
+    out->solve_path = h->solve_path;
     return SGLM_OK;
   }
   out->passes = h->passes;
@@ -1837,6 +2074,14 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->rccl_group = 0;
   out->dev_passes = h->dev_passes;
   out->overlap_chunks = h->ov_chunks();
+  out->comm_path = h->comm.kind == 2   ? SGLM_COMM_RCCL
+                   : h->comm.kind == 1 ? (h->comm.on_device ? SGLM_COMM_CALLER_DEVICE : SGLM_COMM_CALLER_HOST)
+                                       : SGLM_COMM_NONE;
+  out->rank_blocks = h->gather_ranks() ? 1 : 0;
+  out->pass_kernel_ms_min = h->pass_ms;
+  out->proc_chunks = h->nch;
+  out->proc_chunk_rows = h->ch_rows;
+  out->solve_path = h->solve_path;
   return SGLM_OK;
 }
 
@@ -1873,25 +2118,6 @@ int sglm_fit_lm_external(const sglm_backend* be, sglm_allreduce_fn fn, void* com
   return lm_drive(eb, out);
 }
 
-// ---- in-process communicator: N host threads, one handle each (a JVM driver's thread pool) ----
-// Every rank's call blocks until all N have arrived; the last to arrive sums the N buffers in
-// rank order (deterministic, independent of arrival order) and writes the sum into all of them.
-struct sglm_local_comm {
-  int nranks = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t generation = 0;
-  std::vector<double*> bufs;
-  int64_t count = -1;
-  bool failed = false;  // this round: a rank passed another count
-  bool result = false;  // the last completed round failed (read by its waiters only)
-  struct Rank {
-    sglm_local_comm* c;
-    int rank;
-  };
-  std::vector<Rank> ranks;
-};
 
 int sglm_local_comm_create(int nranks, sglm_local_comm** out) {
   if (!out || nranks < 1) {

@@ -40,6 +40,8 @@ hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStrea
 hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,
                               int nrow, double* out, hipStream_t st);
 hipError_t launch_sum_chunks(const double* chunks, int nch, int p, double* out, hipStream_t st);
-hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st);
+hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st, bool full = false);
+// x = A b, A column-major p x p, summed over k in ascending order (the reference's inv * b)
+hipError_t launch_inv_gemv(const double* A, int p, const double* b, double* x, hipStream_t st);
 
 }  // namespace sglm

@@ -593,9 +593,10 @@ __global__ void sum_chunks_kernel(const double* __restrict__ chunks, int nch, in
   }
 }
 
-// Packed lower triangle (row-major) -> column-major p x p lower triangle (for potrf) and X'Wz.
+// Packed lower triangle (row-major) -> column-major p x p lower triangle (for potrf; both
+// triangles when `full`, for getrf) and X'Wz.
 __global__ void unpack_lower_kernel(const double* __restrict__ packed, int p, double* __restrict__ A,
-                                    double* __restrict__ b) {
+                                    double* __restrict__ b, int full) {
   const int64_t tri = (int64_t)p * (p + 1) / 2;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tri + p; e += (int64_t)gridDim.x * blockDim.x) {
     if (e < tri) {
@@ -604,10 +605,25 @@ __global__ void unpack_lower_kernel(const double* __restrict__ packed, int p, do
       while ((i + 1) * (i + 2) / 2 <= e) ++i;
       const int64_t j = e - i * (i + 1) / 2;
       A[i + j * (int64_t)p] = packed[e];
+      if (full) A[j + i * (int64_t)p] = packed[e];
     } else {
       b[e - tri] = packed[e];
     }
   }
+}
+
+// coefs = XtWXi * XtWy (utils.scala:104, 135) from the explicit inverse of the LU route: one
+// thread per coefficient, the product summed over k in ascending order without contraction --
+// the order of the oracle's wls_solve and of the host solver.  Column-major A: the threads of a
+// wave read consecutive elements of column k.
+__global__ void inv_gemv_kernel(const double* __restrict__ A, int p, const double* __restrict__ b,
+                                double* __restrict__ x) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p) return;
+  double s = 0.0;
+  for (int k = 0; k < p; ++k) s += A[i + (int64_t)k * p] * b[k];
+  x[i] = s;
 }
 
 // ---------------------------------------------------------------------------------
@@ -685,11 +701,16 @@ hipError_t launch_sum_chunks(const double* chunks, int nch, int p, double* out, 
   return hipGetLastError();
 }
 
-hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st) {
+hipError_t launch_unpack_lower(const double* packed, int p, double* A, double* b, hipStream_t st, bool full) {
   const int64_t total = (int64_t)p * (p + 1) / 2 + p;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(unpack_lower_kernel, dim3(blocks), dim3(256), 0, st, packed, p, A, b);
+  hipLaunchKernelGGL(unpack_lower_kernel, dim3(blocks), dim3(256), 0, st, packed, p, A, b, full ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_inv_gemv(const double* A, int p, const double* b, double* x, hipStream_t st) {
+  hipLaunchKernelGGL(inv_gemv_kernel, dim3((p + 63) / 64), dim3(64), 0, st, A, p, b, x);
   return hipGetLastError();
 }
 

@@ -180,8 +180,10 @@ class Engine:
         return X, y, m, off, pr
 
     # ---- communicators ----
-    def set_comm(self, fn, on_device: bool):
-        """fn(buf_ptr:int, count:int, stream:int, on_device:bool) -> None, sums in place."""
+    def set_comm(self, fn, on_device: bool, rank=None):
+        """fn(buf_ptr:int, count:int, stream:int, on_device:bool) -> None, sums in place.  With
+        `rank` (this process's rank in fn's group) the scalars are summed in rank order with
+        compensation (sglm_set_comm_rank)."""
         def _cb(ctx, buf, count, stream, dev):
             try:
                 fn(C.cast(buf, C.c_void_p).value, int(count), stream, bool(dev))
@@ -193,6 +195,8 @@ class Engine:
         cb = L.ALLREDUCE_FN(_cb)
         self._comm_keep = cb
         L.check(self._lib.sglm_set_comm(self._h, cb, None, int(bool(on_device))), "sglm_set_comm")
+        if rank is not None:
+            L.check(self._lib.sglm_set_comm_rank(self._h, int(rank)), "sglm_set_comm_rank")
 
     def set_comm_local(self, rank):
         """Join an in-process communicator (distributed.LocalComm(n).rank(r)): host threads of
@@ -291,7 +295,10 @@ class Engine:
     def stats(self) -> dict:
         s = L.Stats()
         L.check(self._lib.sglm_get_stats(self._h, C.byref(s)))
-        return {k: getattr(s, k) for k, _ in L.Stats._fields_}
+        d = {k: getattr(s, k) for k, _ in L.Stats._fields_}
+        d["comm_path_name"] = L.COMM_PATHS.get(d["comm_path"], "?")
+        d["solve_path_name"] = L.SOLVE_PATHS.get(d["solve_path"], "?")
+        return d
 
     def reset_stats(self):
         L.check(self._lib.sglm_reset_stats(self._h))

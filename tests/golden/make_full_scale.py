@@ -8,6 +8,12 @@ the same shards in HBM and compares coefficients / standard errors / deviance at
 the same iteration count, printing the final |delta deviance| beside tol.
 
     python tests/golden/make_full_scale.py [name ...]   ->  tests/golden/full_scale.json
+    python tests/golden/make_full_scale.py --orders       ->  full_scale.json["logit1b"]["orders"]
+
+`--orders` records, beside the compensated trajectory the engine reproduces, the logit1b fit with
+the reference's own summation order for the deviance (plain per-partition running sums, the
+partitions added in order: GLM.scala:168, 404-407) and, to separate the two effects, the same
+8-partition fitMultipleBinomial with compensated sums.
 """
 import json
 import os
@@ -26,12 +32,34 @@ CASES = {
     "poisson64": (2, 0, 125_000_000, 64, 3, "poisson", "log"),         # configs[2] per-GPU shard
     "logit512r": (0, 0, 60_000_000, 512, 5, "binomial", "logit"),      # configs[4] p, resident: the wide path
     "gamma2048": (3, 0, 12_500_000, 2048, 4, "gamma", "inverse"),     # configs[3] per-GPU shard, wide + GPU solve
+    "logit512p": (0, 0, 250_000_000, 512, 5, "binomial", "logit"),     # configs[4] per-GPU shard, procedural X
 }
+PROCEDURAL = {"logit512p"}
+
+
+def orders(out):
+    kind, row0, n, p, seed, fam, link = CASES["logit1b"]
+    res = {}
+    for label, plain in (("reference_order_npart8", True), ("compensated_npart8", False)):
+        t0 = time.time()
+        f = po.fit_glm_synth(kind, row0, n, p, seed, fam, link, nthreads=os.cpu_count() or 8, npart=8,
+                             plain_sums=plain, verbose=True)
+        res[label] = {"npart": 8, "init": "multiple", "plain_sums": plain, "iter": f.iter, "coefs": f.coefs.tolist(),
+                      "stderr": f.stderr.tolist(), "deviance": f.deviance, "dev_trace": f.dev_trace.tolist(),
+                      "oracle_seconds": round(time.time() - t0, 1)}
+        print(f"logit1b {label}: {f.iter} iterations, deltas {[b - a for a, b in zip(f.dev_trace, f.dev_trace[1:])]}",
+              flush=True)
+    out["logit1b"]["orders"] = res
 
 
 def main(names):
     path = os.path.join(HERE, "full_scale.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
+    if names == ["--orders"]:
+        orders(out)
+        with open(path, "w") as fh:
+            json.dump(out, fh, indent=1)
+        return
     for name in names or list(CASES):
         kind, row0, n, p, seed, fam, link = CASES[name]
         t0 = time.time()
@@ -41,7 +69,7 @@ def main(names):
                      "tol": 1e-6, "init": "single", "iter": f.iter, "coefs": f.coefs.tolist(),
                      "stderr": f.stderr.tolist(), "deviance": f.deviance, "null_deviance": f.null_deviance,
                      "pearson": f.pearson, "loglik": f.loglik, "dev_trace": f.dev_trace.tolist(),
-                     "oracle_seconds": round(dt, 1)}
+                     "oracle_seconds": round(dt, 1), "procedural": name in PROCEDURAL}
         print(f"{name}: {f.iter} iterations, deviance {f.deviance!r}, {dt:.0f} s", flush=True)
         with open(path, "w") as fh:
             json.dump(out, fh, indent=1)

@@ -5,7 +5,7 @@ oracle -- at the bench's own full sizes where the streaming oracle pins them.
   configs[1]  100M x 256 logit (fused pass irls_pass_kernel<16>)   -- full size, full_scale.json
   configs[2]  Poisson/log + offset + prior at p = 64 (irls_narrow_kernel<4>) -- 200k rows here,
               the 125M-row per-GPU shard at full size (full_scale.json)
-  configs[3]  Gamma/inverse at p = 2048 (16 panels, rocSOLVER Cholesky)
+  configs[3]  Gamma/inverse at p = 2048 (16 panels, rocSOLVER LU + explicit inverse)
   north star  1B x 32 logit on one GPU (irls_narrow_kernel<2>)     -- full size, full_scale.json
 
 Bar (north_star): coefficients, standard errors, deviance within 1e-9 relative, identical
@@ -61,20 +61,29 @@ def test_config2_poisson_offset_prior_p64(eng):
     assert rel(f.dev_trace, o.dev_trace) < TOL
 
 
+# configs[3]'s conditioning floor (oracle/lu_floor.py, tests/golden/lu_floor_p2048.json): on the
+# oracle's OWN X'WX of the last solve (cond 3.3e5 at 6000 rows, ~1e6-1e7 at 12.5M), LAPACK's dgetrf +
+# dgetri -- Breeze inv's algorithm as netlib-java binds it natively -- lands up to 1.6e-9 from the
+# oracle's unblocked restatement of the same algorithm, the product inv * X'Wz summed in another order
+# 2.0e-9, and X'WX re-summed in another order (2.4e-16 norm-wise) 2.8e-9: the smallest coefficients
+# (|b| ~ 0.02 beside max ~ 50) are defined only to a few 1e-9 by the reference itself.  Bar: 1e-9
+# norm-wise for the coefficients (all other outputs elementwise) and WIDE_FLOOR elementwise.
+WIDE_FLOOR = 2e-8
+
+
 def test_config3_gamma_p2048(eng):
     """BASELINE configs[3]'s family / design at p = 2048: all 16 column panels of the wide
-    Gram kernel and the device (rocSOLVER) Cholesky + inverse, vs the oracle's LU inverse."""
+    Gram kernel and the device (rocSOLVER) LU + explicit inverse, vs the oracle's LU inverse."""
     n, p = 6000, 2048
     eng.synth(3, 777, n, p, 4)
     f = eng.fit_glm("gamma", "inverse")
     st = eng.stats()
-    assert st["path"] == 1 and st["wide_panels"] == 16
+    assert st["path"] == 1 and st["wide_panels"] == 16 and st["solve_path_name"] == "device-lu"
     o = po.fit_glm_synth(3, 777, n, p, 4, "gamma", "inverse", nthreads=16)
     assert f.iter == o.iter
-    # cond(X'WX) ~1e6-1e7 here: the smallest coefficients (|b| ~ 0.03 beside max |b| ~ 11) move by
-    # ~2e-9 relative under ANY change of solve algorithm -- Cholesky vs the reference's LU on the
-    # oracle's own X'WX gives 1.85e-9 -- so coefficients are bounded norm-wise, the rest elementwise
-    assert nrel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    print(f"\nconfigs[3] 6000 x 2048: coefs elementwise {rel(f.coefs, o.coefs):.2e}, norm-wise "
+          f"{nrel(f.coefs, o.coefs):.2e}; stderr {rel(f.stderr, o.stderr):.2e}")
+    assert nrel(f.coefs, o.coefs) < TOL and rel(f.coefs, o.coefs) < WIDE_FLOOR and rel(f.stderr, o.stderr) < TOL
     assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
                [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL
 
@@ -95,17 +104,44 @@ def test_full_scale_fit_matches_streaming_oracle(eng, name):
     (tests/golden/make_full_scale.py): GLM.scala:452-462's absolute tol 1e-6 on a deviance of
     up to ~1.3e9 decides the iteration count, so the final |delta deviance| is printed beside it."""
     c = FULL[name]
-    eng.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"])
+    eng.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"], procedural=c.get("procedural", False))
     f = eng.fit_glm(c["family"], c["link"], tol=c["tol"])
     tr = np.asarray(c["dev_trace"])
     print(f"\n{name}: iter {f.iter} (oracle {c['iter']}); final |delta dev| engine "
           f"{abs(f.dev_trace[-1] - f.dev_trace[-2]):.3e} oracle {abs(tr[-1] - tr[-2]):.3e} vs tol {c['tol']:.0e}; "
           f"previous {abs(f.dev_trace[-2] - f.dev_trace[-3]):.3e}")
     assert f.iter == c["iter"]
-    # gamma/inverse at p = 2048 is ill-conditioned (DESIGN.md section 3): coefficients norm-wise
+    # gamma/inverse at p = 2048 is ill-conditioned (WIDE_FLOOR above): coefficients norm-wise at 1e-9
+    # and elementwise at the floor
     ec = nrel(f.coefs, c["coefs"]) if c["family"] == "gamma" else rel(f.coefs, c["coefs"])
+    print(f"coefs elementwise {rel(f.coefs, c['coefs']):.2e}")
     assert ec < TOL and rel(f.stderr, c["stderr"]) < TOL, (ec, rel(f.stderr, c["stderr"]))
+    assert rel(f.coefs, c["coefs"]) < WIDE_FLOOR
     assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
                [c["deviance"], c["null_deviance"], c["pearson"], c["loglik"]]) < TOL
     assert rel(f.dev_trace, tr) < TOL
     eng.synth(c["kind"], 0, 64, c["p"], c["seed"])  # release the full-size shard
+
+
+@pytest.mark.skipif("logit1b" not in FULL, reason="full_scale.json has no logit1b")
+def test_logit1b_over_eight_shards_matches_one_shard():
+    """SURVEY 8(e) determinism at the north star's size: the full 1B x 32 logit design split into 8
+    row shards on the one GPU (a multi-device handle listing device 0 eight times: shard partials
+    summed on the host in shard order, the scalars -- deviance first -- in rank blocks with
+    compensation) converges like the one-shard fit and the streaming oracle: same 4 iterations,
+    the deviance trajectory within 1e-9 (GLM.scala:452's absolute tol 1e-6 sits at ~4 ulp of the
+    1.33e9 deviance here)."""
+    c = FULL["logit1b"]
+    with Engine(devices=[0] * 8) as g:
+        g.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"])
+        f = g.fit_glm(c["family"], c["link"], tol=c["tol"])
+        st = g.stats()
+    tr = np.asarray(c["dev_trace"])
+    print(f"\nlogit1b over 8 shards: iter {f.iter} (oracle {c['iter']}); deltas "
+          f"{np.diff(f.dev_trace).tolist()} vs oracle {np.diff(tr).tolist()}")
+    assert st["ndev"] == 8 and st["rank_blocks"] == 1 and st["comm_path_name"] == "group-host"
+    assert f.iter == c["iter"]
+    assert rel(f.coefs, c["coefs"]) < TOL and rel(f.stderr, c["stderr"]) < TOL
+    assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
+               [c["deviance"], c["null_deviance"], c["pearson"], c["loglik"]]) < TOL
+    assert rel(f.dev_trace, tr) < TOL

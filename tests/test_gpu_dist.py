@@ -33,7 +33,7 @@ def _worker(rank, world, port, mode, q):
     eng.set_data(X, y, offset=off, prior=pr)
     if mode == "gloo":
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        eng.set_comm(D.torch_allreduce(), on_device=False)
+        eng.set_comm(D.torch_allreduce(), on_device=False, rank=rank)
     elif mode == "rccl":
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         uid = [Engine.rccl_unique_id() if rank == 0 else None]
@@ -42,7 +42,7 @@ def _worker(rank, world, port, mode, q):
     else:  # torch nccl group, device buffers
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        eng.set_comm(D.torch_allreduce(), on_device=True)
+        eng.set_comm(D.torch_allreduce(), on_device=True, rank=rank)
     f = eng.fit_glm("poisson", "log", init="multiple")
     q.put((rank, (f.coefs, f.stderr, np.array([f.deviance, f.null_deviance, f.pearson, f.loglik, f.iter, f.nrow,
                                                 f.npart]))))

@@ -64,6 +64,29 @@ def test_incomplete_or_mismatched_upload_is_refused(eng):
     assert f.iter == o.iter and rel(f.coefs, o.coefs) < TOL
 
 
+def test_overlapping_blocks_are_refused(eng):
+    """a repeated or overlapping block must not count its rows twice -- two
+    set_rows(0, n/2) calls would otherwise pass the coverage check with the second half never
+    written (zero X, y) and the fit would silently run over it."""
+    n, p = 1000, 5
+    X, y, _, _ = synth.generate(0, 0, n, p, 3)
+    eng.reserve(n, p)
+    eng.set_rows(0, X[:500], y[:500])
+    with pytest.raises(L.IllegalArgumentException, match="overlap"):
+        eng.set_rows(0, X[:500], y[:500])             # the same block again
+    with pytest.raises(L.IllegalArgumentException, match="overlap"):
+        eng.set_rows(499, X[499:700], y[499:700])     # straddles the written block's end
+    eng.set_rows(700, X[700:], y[700:])
+    with pytest.raises(L.IllegalArgumentException, match="overlap"):
+        eng.set_rows(600, X[600:701], y[600:701])     # straddles the next block's start
+    with pytest.raises(L.IllegalArgumentException, match="never written"):
+        eng.fit_glm()
+    eng.set_rows(500, X[500:700], y[500:700])         # the exact gap
+    f = eng.fit_glm()
+    o = po.fit_glm(X, y)
+    assert f.iter == o.iter and rel(f.coefs, o.coefs) < TOL
+
+
 def test_predict_new_keeps_the_training_design_resident(eng):
     X, y, off, pr = synth.generate(2, 0, 30_000, 12, 5)
     eng.set_data(X, y, offset=off, prior=pr)

@@ -116,3 +116,20 @@ def test_capped_fits_speculate_identically(max_iter):
     (f1, k1), (f0, k0) = res
     assert k0 == 0 and (k1 == 0 if max_iter else k1 >= 1)
     _same(f1, f0)
+
+
+def test_default_overlapped_wide_pass_speculates_identically():
+    """the overlapped wide pass at the DEFAULT chunking (SGLM_WIDE_OV_MIN = 65536 rows:
+    >= 2 * ov_min rows give several chunks, the banded schedule over each) runs its deviance-only
+    pass through the same chunk reduces -- bitwise the full pass's fit."""
+    on, off = _engine(True), _engine(False)
+    try:
+        f1, k1 = _fit(on, 0, 262_144, 300, 13, "binomial", "logit")
+        ch = on.stats()["overlap_chunks"]
+        f0, k0 = _fit(off, 0, 262_144, 300, 13, "binomial", "logit")
+    finally:
+        on.close()
+        off.close()
+    print(f"\nwide p300 default chunks {ch}: iter {f1.iter}, deviance-only passes {k1}")
+    assert ch >= 2 and k0 == 0 and k1 >= 1
+    _same(f1, f0)

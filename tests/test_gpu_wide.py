@@ -228,3 +228,50 @@ def test_procedural_lm_and_get_data(eng):
     assert rel(f.coefs, r["coefs"]) < TOL and rel(f.stderr, r["stderr"]) < TOL
     with pytest.raises(Exception):
         eng.get_data()
+
+
+def _engine_env(**env) -> Engine:
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Engine(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("kind,p,fam,link", [(0, 300, "binomial", "logit"), (3, 520, "gamma", "inverse")])
+def test_wide_solve_lu_and_cholesky(kind, p, fam, link):
+    """The wide path's device solve: by default the reference's own algorithm, LU + explicit
+    inverse (Breeze inv = dgetrf + dgetri, utils.scala:103-105) by rocSOLVER with coefs = inv * X'Wz
+    summed in the reference's order; SGLM_WIDE_SOLVE=chol the Cholesky route.  Both against the
+    oracle's LU at 1e-9, and sglm_stats.solve_path says which ran."""
+    n = 20_000
+    X, y, _, _ = synth.generate(kind, 0, n, p, 17)
+    o = po.fit_glm(X, y, fam, link, nthreads=8)
+    for mode, want in (("lu", "device-lu"), ("chol", "device-cholesky")):
+        e = _engine_env(SGLM_WIDE_SOLVE=mode)
+        try:
+            e.synth(kind, 0, n, p, 17)
+            f = e.fit_glm(fam, link)
+            st = e.stats()
+        finally:
+            e.close()
+        assert st["path"] == 1 and st["solve_path_name"] == want, st["solve_path_name"]
+        assert f.iter == o.iter, mode
+        assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL, (mode, rel(f.coefs, o.coefs))
+        assert rel(f.deviance, o.deviance) < TOL
+
+
+def test_wide_singular_gram_raises_matrix_singular(weng):
+    """An exactly singular X'WX (a duplicated column) on the device LU route -> Breeze's
+    MatrixSingularException, as inv() throws it (utils.scala:103)."""
+    from sparkglm_amd import _lib as L
+    X, y, _, _ = synth.generate(1, 0, 5000, 6, 3)
+    X = np.column_stack([X, X[:, 2]])
+    weng.set_data(X, y)
+    with pytest.raises(L.MatrixSingularException):
+        weng.fit_lm()

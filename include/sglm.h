@@ -86,8 +86,9 @@ enum sglm_init {
 enum sglm_solve_path {
   SGLM_SOLVE_HOST_CHOL = 0,   /* host Cholesky (p <= 256, well conditioned) */
   SGLM_SOLVE_HOST_LU = 1,     /* host LU + explicit inverse: Breeze inv (utils.scala:103-105) */
-  SGLM_SOLVE_DEVICE_CHOL = 2, /* wide p, SGLM_WIDE_SOLVE=chol: rocSOLVER potrf / potrs / potri */
-  SGLM_SOLVE_DEVICE_LU = 3    /* wide p (default): rocSOLVER getrf + getri, coefs = inv * X'Wz */
+  SGLM_SOLVE_DEVICE_CHOL = 2, /* wide p (default): rocSOLVER potrf / potrs / potri */
+  SGLM_SOLVE_DEVICE_LU = 3    /* wide p, SGLM_WIDE_SOLVE=lu (or ill-conditioned above p = 1024):
+                                 rocSOLVER getrf + getri, coefs = inv * X'Wz */
 };
 
 /* Where a pass's all-reduce ran (sglm_stats.comm_path). */

@@ -22,6 +22,13 @@ enum PassMode : int {
 enum Family : int { FAM_BINOMIAL = 0, FAM_GAUSSIAN = 1, FAM_POISSON = 2, FAM_GAMMA = 3 };
 enum Link : int { LNK_LOGIT = 0, LNK_PROBIT = 1, LNK_CLOGLOG = 2, LNK_IDENTITY = 3, LNK_LOG = 4, LNK_INVERSE = 5 };
 
+// Which families carry their final statistics in the narrow pass (PassArgs::stats_in_pass;
+// rowmath.hpp pass_row_stats): binomial / logit (without m), Poisson / log, Gamma / inverse.
+constexpr bool stats_in_pass_family(int fam, int lnk) {
+  return (fam == FAM_BINOMIAL && lnk == LNK_LOGIT) || (fam == FAM_POISSON && lnk == LNK_LOG) ||
+         (fam == FAM_GAMMA && lnk == LNK_INVERSE);
+}
+
 // Largest column-block count of the fused (single-panel) kernel: p <= 16*16 = 256.
 constexpr int MAX_P16 = 16;
 

@@ -168,6 +168,8 @@ struct sglm_engine : public Backend {
   Comm comm;
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
+  double stats_const = 0.0;    // the fit's initial-pass S_AUX2: constant part of in-pass Poisson / Gamma statistics
+  bool stats_every_pass = false;  // SGLM_STATS_EVERY_PASS=1: Poisson / Gamma statistics in every pass (A/B)
   bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
   // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
   // scalar reduction but no Gram -- bitwise the scalars of the full pass.  SGLM_SPECULATE=0 off.
@@ -214,9 +216,9 @@ struct sglm_engine : public Backend {
   bool has_sched[2] = {false, false};
   hipEvent_t evm = nullptr;
   rocblas_handle blas = nullptr;
-  // wide-path device solve (SGLM_WIDE_SOLVE): 1 LU + explicit inverse (Breeze inv: dgetrf + dgetri,
-  // utils.scala:103-105), 0 Cholesky (potrf / potrs / potri)
-  int wide_lu = 1;
+  // wide-path device solve (SGLM_WIDE_SOLVE): 0 Cholesky (potrf / potrs / potri, the default),
+  // 1 LU + explicit inverse (Breeze inv's algorithm: dgetrf + dgetri, utils.scala:103-105)
+  int wide_lu = 0;
   int64_t proc_scratch_max = 0;  // SGLM_PROC_SCRATCH_MAX (GiB): cap on the procedural chunk scratch (0: none)
   // stats
   int64_t passes = 0, dev_passes = 0;
@@ -942,7 +944,29 @@ struct sglm_engine : public Backend {
     }
     if (R) compensated_rank_sum(hred + plen, R, NS, hred + sc);
     std::memcpy(packed, hred, sizeof(double) * plen);
+    finish_scalars(mode, family, packed + sc);
     return SGLM_OK;
+  }
+
+  // The narrow pass's in-pass Poisson / Gamma statistics lack their per-fit constants (rowmath.hpp
+  // init_stats_const), which the fit's initial pass sums into S_AUX2: kept here, applied to every
+  // later pass that carried the statistics -- R's dpois loglik sum pw (y log mu - mu) minus
+  // sum pw lgamma(y + 1); Gamma's S_LL = sum pw log y and S_AUX1 = sum pw log mu = sum pw log y -
+  // sum pw log(y eta).  Applied once, on the all-reduced scalars.
+  void finish_scalars(int mode, int family, double* s) {
+    if (family != FAM_POISSON && family != FAM_GAMMA) return;
+    if (mode == MODE_INIT_SINGLE || mode == MODE_INIT_MULTI) {
+      stats_const = s[S_AUX2];
+      s[S_AUX2] = 0.0;
+      return;
+    }
+    if (mode != MODE_IRLS || !pass_has_stats()) return;
+    if (family == FAM_POISSON) {
+      s[S_LL] -= stats_const;
+    } else {
+      s[S_LL] = stats_const;
+      s[S_AUX1] = stats_const - s[S_AUX1];
+    }
   }
 
   // Kernel times of the pass just synchronised (HIP events on this engine's stream).
@@ -1005,9 +1029,15 @@ struct sglm_engine : public Backend {
     a.ybar = ybar;
     a.partials = dpart;
     a.stride = stride;
-    // binomial / logit (m = 1) on the narrow path: final statistics in the pass, no eta store
-    a.stats_in_pass = (narrow && mode == MODE_IRLS && family == FAM_BINOMIAL && link == LNK_LOGIT && !dm &&
-                       !force_eta_store) ? 1 : 0;
+    // Final statistics in the narrow pass, no eta store (rowmath.hpp stats_in_pass_family):
+    // binomial / logit (m = 1) in every IRLS pass -- measured faster than the lean variant, the
+    // statistics hide under the stream (DESIGN 4 K1') -- and Poisson / Gamma in the deviance-only
+    // pass only, the pass glm_drive predicts to end the fit: at p = 64 their statistics rows cost
+    // +14 % per pass (125M x 64 Poisson: 17.4 against 15.3 ms, tools/ab_stats.py; the family
+    // arithmetic runs on 16 of 64 lanes there), while the deviance-only pass has no Gram to slow.
+    a.stats_in_pass = (narrow && mode == MODE_IRLS && stats_in_pass_family(family, link) &&
+                       !(family == FAM_BINOMIAL && dm) && !force_eta_store &&
+                       (family == FAM_BINOMIAL || dev_only || stats_every_pass)) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
     a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
@@ -1224,6 +1254,7 @@ struct sglm_engine : public Backend {
       subs[0]->red_on_device = false;
       comm.ms += now_ms() - t0;
     }
+    finish_scalars(mode, family, packed + sc);
     return SGLM_OK;
   }
 
@@ -1293,16 +1324,22 @@ struct sglm_engine : public Backend {
 
 // =====================================================================================
 // Device solver for wide p, from the reduced buffer on the GPU.
-// Default: the reference's own algorithm -- LU with partial pivoting and the explicit inverse
-// (Breeze inv = LAPACK dgetrf + dgetri, utils.scala:103-105, 134-136) by rocSOLVER, then
-// coefs = inv * X'Wz summed in the reference's order (inv_gemv_kernel) and stdErr from diag(inv).
-// SGLM_WIDE_SOLVE=chol: Cholesky (potrf / potrs, potri for the standard errors), switching to the
-// LU route when potrf rejects the matrix or its pivots flag it ill-conditioned (solve.hpp).
-// Exact singularity (a zero pivot of dgetrf) -> MatrixSingularException, as Breeze's inv.
-// Either algorithm is within the reference's own spread: on the same X'WX, LAPACK's blocked
-// dgetrf/dgetri and an unblocked restatement part by ~cond * eps (oracle/lu_floor.py).
+// Default: Cholesky (rocSOLVER potrf / potrs, potri for the standard errors).  A matrix potrf
+// rejects or whose pivots flag it ill-conditioned (solve.hpp LU_SWITCH_RATIO) takes the
+// reference's own algorithm, LU with partial pivoting and the explicit inverse (Breeze inv =
+// LAPACK dgetrf + dgetri, utils.scala:103-105, 134-136): on the host -- the oracle's unblocked
+// order, as the narrow path -- up to p = HOST_LU_MAX_P, by rocSOLVER getrf / getri above it (a
+// host LU at p = 2048 is ~10 s).  SGLM_WIDE_SOLVE=lu runs the rocSOLVER LU route always, coefs =
+// inv * X'Wz summed in the reference's order (inv_gemv_kernel), stdErr from diag(inv).
+// Measured against the oracle's unblocked LU (tests/test_gpu_wide.py, oracle/lu_floor.py):
+// Cholesky lands closer than rocSOLVER's blocked getrf + getri on ill-conditioned gamma designs
+// (p = 520, cond ~1e7: 1e-9 against 1e-7 elementwise on the smallest coefficient), which is why
+// it stays the default; norm-wise both agree to ~1e-12.  Exact singularity (a zero pivot of
+// dgetrf) -> MatrixSingularException, as Breeze's inv.
 // =====================================================================================
 namespace {
+
+constexpr int64_t HOST_LU_MAX_P = 1024;
 
 struct DeviceSolver : public SolverIface {
   sglm_engine* e;
@@ -1310,9 +1347,12 @@ struct DeviceSolver : public SolverIface {
   double *dA = nullptr, *dB = nullptr, *dAi = nullptr, *dpk = nullptr, *dx = nullptr;
   rocblas_int *dinfo = nullptr, *dipiv = nullptr;
   std::vector<double> ldiag;
-  int kind = 0;  // 0 none, 1 Cholesky factor in dA, 2 explicit inverse in dA (LU route)
+  std::unique_ptr<HostSolver> host;
+  int kind = 0;  // 0 none, 1 Cholesky factor in dA, 2 explicit inverse in dA (LU route), 3 host solver
   DeviceSolver(sglm_engine* eng, int64_t pp) : e(eng), p(pp) {}
-  int path() const override { return kind == 1 ? SGLM_SOLVE_DEVICE_CHOL : kind == 2 ? SGLM_SOLVE_DEVICE_LU : -1; }
+  int path() const override {
+    return kind == 1 ? SGLM_SOLVE_DEVICE_CHOL : kind == 2 ? SGLM_SOLVE_DEVICE_LU : kind == 3 ? host->path() : -1;
+  }
   ~DeviceSolver() override {
     (void)hipSetDevice(e->device);
     for (double* ptr : {dA, dB, dAi, dpk, dx})
@@ -1370,7 +1410,12 @@ struct DeviceSolver : public SolverIface {
       }
       if (r < LU_SWITCH_RATIO) info = -1;  // ill-conditioned: the reference's LU inverse
     }
-    if (info != 0) return solve_lu(src, x);  // not positive definite / ill-conditioned
+    if (info != 0) {  // not positive definite / ill-conditioned: the reference's LU inverse
+      if (p > HOST_LU_MAX_P) return solve_lu(src, x);
+      if (!host) host = std::make_unique<HostSolver>(p);
+      kind = 3;
+      return host->solve(packed, x);
+    }
     if (rocsolver_dpotrs(e->blas, rocblas_fill_lower, (rocblas_int)p, 1, dA, (rocblas_int)p, dB, (rocblas_int)p) !=
         rocblas_status_success) {
       set_error("rocsolver_dpotrs failed");
@@ -1420,6 +1465,7 @@ struct DeviceSolver : public SolverIface {
     return SGLM_OK;
   }
   int inv_diag(double* d) override {
+    if (kind == 3) return host->inv_diag(d);
     if (kind == 0) {
       for (int64_t i = 0; i < p; ++i) d[i] = 0.0;
       return SGLM_OK;
@@ -1433,6 +1479,7 @@ struct DeviceSolver : public SolverIface {
     return SGLM_OK;
   }
   int inverse(double* Ainv) override {
+    if (kind == 3) return host->inverse(Ainv);
     if (kind == 0) return SGLM_OK;
     HIPCHK(hipSetDevice(e->device));
     if (kind == 1)
@@ -1583,6 +1630,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
   if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
+  if (const char* se = std::getenv("SGLM_STATS_EVERY_PASS")) h->stats_every_pass = std::atoi(se) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
@@ -1591,7 +1639,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
-  if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "chol") != 0;
+  if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "lu") == 0;
   if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
   *out = h;
   return SGLM_OK;

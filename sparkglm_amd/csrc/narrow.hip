@@ -204,9 +204,12 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 
 // IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
 // IRLS = false instantiation, so the iterations' main loop carries none of their branches.
-// STATS (binomial / logit IRLS without m, PassArgs::stats_in_pass): the pass also accumulates
-// pearsonCalc / llBinomial at this pass's mu and stores no eta -- the last pass of a fit then
-// carries the final statistics (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass).
+// STATS (PassArgs::stats_in_pass: binomial / logit IRLS without m, Poisson / log, Gamma /
+// inverse): the pass also accumulates the final statistics -- pearsonCalc / llBinomial, the R
+// families' loglik ingredients -- at this pass's mu and stores no eta; the last pass of a fit then
+// carries them (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass, ~1 % at p = 64).
+// The Poisson / Gamma statistics' per-fit constants (rowmath.hpp init_stats_const) are summed by
+// the initial pass (IRLS = false) into S_AUX2.
 template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
@@ -223,6 +226,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   constexpr bool irls = IRLS;
   const int mode = IRLS ? (int)MODE_IRLS : a.mode;
   const bool has_eta = irls && !STATS && a.eta_out != nullptr;
+  // the initial pass of a Poisson / Gamma fit sums the in-pass statistics' constants (S_AUX2)
+  constexpr bool INIT_CONST = !IRLS && (FAM == FAM_POISSON || FAM == FAM_GAMMA);
+  constexpr bool XS = STATS || INIT_CONST;  // the extra scalar accumulators are live
+  using SL = StatsSlots<FAM>;
 
   // per-lane parts of the DMA source addresses: lane -> (column cc of the group, row pair j);
   // the swizzle repeats every LPER column groups
@@ -334,10 +341,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           const double y = hi ? y_p : yv, m = hi ? m_p : mv, off = hi ? off_p : ov, pw = hi ? pw_p : pv;
           if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = et * w; s_dev += w; }
           else if constexpr (STATS)
-            pass_row_logit_stats(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
+            pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
           else
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                      !IRLS);
+          if constexpr (INIT_CONST)
+            if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
         }
       }
       // w / w*z at [half * NRB + rl]: the stashed block in the upper half
@@ -423,10 +432,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
         else if constexpr (STATS)
-          pass_row_logit_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
+          pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
         else
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
                    !IRLS);
+        if constexpr (INIT_CONST)
+          if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;
@@ -580,7 +591,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   for (int o = 1; o < 64; o <<= 1) {
     s_dev += __shfl_xor(s_dev, o);
     s_aux += __shfl_xor(s_aux, o);
-    if constexpr (STATS) {
+    if constexpr (XS) {
       s_pear += __shfl_xor(s_pear, o);
       s_ll += __shfl_xor(s_ll, o);
       s_bad += __shfl_xor(s_bad, o);
@@ -623,7 +634,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       for (int b = 0; b < P16; ++b) xz[b] += reg[G::T * 256 + 16 * b + (lane & 15)];
       s_dev += reg[G::T * 256 + G::NC];
       s_aux += reg[G::T * 256 + G::NC + 1];
-      if constexpr (STATS) {
+      if constexpr (XS) {
         s_pear += reg[G::T * 256 + G::NC + 2];
         s_ll += reg[G::T * 256 + G::NC + 3];
         s_bad += reg[G::T * 256 + G::NC + 4];
@@ -660,21 +671,25 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
       for (int b = 0; b < P16; ++b) out[G::T * 256 + 16 * b + lane] = xz[b];
     }
-    if (lane < NS)
-      out[G::T * 256 + G::NC + lane] = lane == S_DEV       ? s_dev
-                                       : lane == S_SUMW    ? s_aux
-                                       : lane == S_PEARSON ? s_pear
-                                       : lane == S_LL      ? s_ll
-                                       : lane == S_BAD     ? s_bad
-                                                           : 0.0;
+    if (lane < NS) {
+      double v = lane == S_DEV ? s_dev : lane == S_SUMW ? s_aux : 0.0;
+      if constexpr (STATS) {
+        if (lane == SL::S2) v = s_pear;
+        if (lane == SL::S3) v = s_ll;
+        if (lane == SL::S4) v = s_bad;
+      }
+      if constexpr (INIT_CONST)
+        if (lane == S_AUX2) v = s_ll;
+      out[G::T * 256 + G::NC + lane] = v;
+    }
   }
 }
 
 template <int P16, int FAM, int LNK>
 void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st) {
-  if (a.mode == MODE_IRLS && FAM == FAM_BINOMIAL && LNK == LNK_LOGIT && a.stats_in_pass && !a.m)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, FAM == FAM_BINOMIAL && LNK == LNK_LOGIT>), gr, bl, 0, st,
-                       a);
+  constexpr bool SP = stats_in_pass_family(FAM, LNK);
+  if (a.mode == MODE_IRLS && SP && a.stats_in_pass && !(FAM == FAM_BINOMIAL && a.m))
+    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, SP>), gr, bl, 0, st, a);
   else if (a.mode == MODE_IRLS)
     hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true>), gr, bl, 0, st, a);
   else

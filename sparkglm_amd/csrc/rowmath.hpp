@@ -413,6 +413,33 @@ __device__ __forceinline__ void stats_row(int fam, int lnk, int mode, double eta
   for (int k = 0; k < NS; ++k) acc.s[k] += r.s[k];
 }
 
+// Rows outside the in-pass statistics' fast ranges: both reference-order functions and the
+// family's statistics slots (s2, s3, s4: StatsSlots), in ONE out-of-line call -- two calls (or
+// an inlined lgamma) around the kernel's live Gram accumulators made the compiler spill them.
+struct RowStats {
+  double w, wz, dev, s2, s3, s4;
+};
+__device__ __noinline__ RowStats stats_row_fallback(int fam, int lnk, double eta, double y, double off, double pw) {
+  const RowWZ r = pass_row_ref(fam, lnk, MODE_IRLS, eta, y, 1.0, off, pw, 0.0);
+  const RowAcc a = stats_row_ref(fam, lnk, MODE_IRLS, eta, y, 1.0, pw, 0.0, false);
+  RowStats o;
+  o.w = r.w;
+  o.wz = r.wz;
+  o.dev = r.dev;
+  o.s2 = a.s[S_PEARSON];
+  if (fam == FAM_BINOMIAL) {
+    o.s3 = a.s[S_LL];
+    o.s4 = a.s[S_BAD];
+  } else if (fam == FAM_POISSON) {
+    o.s3 = a.s[S_LL] + pw * lgamma(y + 1.0);  // the constant part is subtracted once per fit
+    o.s4 = 0.0;
+  } else {
+    o.s3 = a.s[S_AUX0];
+    o.s4 = a.s[S_LL] - a.s[S_AUX1];  // pw log y - pw log mu = pw log(y / mu)
+  }
+  return o;
+}
+
 __device__ __forceinline__ void pass_row_logit_stats(double eta, double y, double off, double pw, double& w, double& wz,
                                                      double& s_dev, double& s_aux, double& s_pear, double& s_ll,
                                                      double& s_bad, bool small_exp) {
@@ -431,15 +458,108 @@ __device__ __forceinline__ void pass_row_logit_stats(double eta, double y, doubl
     s_ll += pw * ((int)y == 1 ? -L : -L - eta);
     return;
   }
-  const RowWZ r = pass_row_ref(FAM_BINOMIAL, LNK_LOGIT, MODE_IRLS, eta, y, 1.0, off, pw, 0.0);
+  const RowStats r = stats_row_fallback(FAM_BINOMIAL, LNK_LOGIT, eta, y, off, pw);
   w = r.w;
   wz = r.wz;
   s_dev += r.dev;
   s_aux += pw;
-  const RowAcc a = stats_row_ref(FAM_BINOMIAL, LNK_LOGIT, MODE_IRLS, eta, y, 1.0, pw, 0.0, false);
-  s_pear += a.s[S_PEARSON];
-  s_ll += a.s[S_LL];
-  s_bad += a.s[S_BAD];
+  s_pear += r.s2;
+  s_ll += r.s3;
+  s_bad += r.s4;
 }
+
+// Poisson / log, in-pass final statistics: pass_row's fast path plus pearsonCalc (R's variance
+// V = mu) and the mu-dependent part of R's dpois log-density, y log mu - mu with
+// log mu = eta.  The per-row constant -lgamma(y + 1) does not depend on the fit: the initial pass
+// sums pw lgamma(y + 1) once into S_AUX2 (init_stats_const) and the engine subtracts it.
+// Slots: s2 = Pearson, s3 = loglik part, s4 unused.
+__device__ __forceinline__ void pass_row_poisson_stats(double eta, double y, double off, double pw, double& w,
+                                                       double& wz, double& s_dev, double& s_aux, double& s2,
+                                                       double& s3, bool small_exp) {
+  if (fabs(eta) < 700.0 && y >= 0.0 && y < 1e300) {
+    const double mu = small_exp ? exp_small(eta) : exp(eta);
+    w = pw * mu;
+    wz = pw * (mu * (eta - off) + (y - mu));
+    s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
+    s_aux += pw;
+    const double r = y - mu;
+    s2 += pw * (r * r) * rcp_pos(mu);
+    s3 += pw * (y * eta - mu);
+    return;
+  }
+  const RowStats r = stats_row_fallback(FAM_POISSON, LNK_LOG, eta, y, off, pw);
+  w = r.w;
+  wz = r.wz;
+  s_dev += r.dev;
+  s_aux += pw;
+  s2 += r.s2;
+  s3 += r.s3;
+}
+
+// Gamma / inverse, in-pass final statistics: pass_row's fast path plus pearsonCalc (V = mu^2:
+// (y - mu)^2 / mu^2 = (y - mu)^2 eta^2) and R's Gamma loglik ingredients sum pw y / mu = sum pw y eta
+// (S_AUX0) and sum pw log mu = sum pw log y - sum pw log(y eta) (S_AUX1: the pass sums the second
+// term, which its deviance already evaluates; the fit-constant sum pw log y -- also S_LL itself --
+// comes from the initial pass, init_stats_const).  Slots: s2 = Pearson, s3 = AUX0, s4 = log(y eta).
+__device__ __forceinline__ void pass_row_gamma_stats(double eta, double y, double off, double pw, double& w,
+                                                     double& wz, double& s_dev, double& s_aux, double& s2, double& s3,
+                                                     double& s4) {
+  if (eta > 1e-150 && eta < 1e150 && y > 1e-150 && y < 1e150) {
+    const double mu = rcp_pos(eta);
+    const double mu2 = mu * mu;
+    const double ye = y * eta;
+    const double L = log_pos(ye);
+    w = pw * mu2;
+    wz = pw * (mu2 * (eta - off) - (y - mu));
+    s_dev += pw * (-(L - (ye - 1.0)));
+    s_aux += pw;
+    const double r = y - mu;
+    s2 += pw * (r * r) * (eta * eta);
+    s3 += pw * ye;
+    s4 += pw * L;
+    return;
+  }
+  const RowStats r = stats_row_fallback(FAM_GAMMA, LNK_INVERSE, eta, y, off, pw);
+  w = r.w;
+  wz = r.wz;
+  s_dev += r.dev;
+  s_aux += pw;
+  s2 += r.s2;
+  s3 += r.s3;
+  s4 += r.s4;
+}
+
+// The per-fit constants of the in-pass statistics, summed by the initial pass into S_AUX2:
+// Poisson sum pw lgamma(y + 1) (R's dpois), Gamma sum pw log y (R's dgamma).
+__device__ __noinline__ double init_stats_const_ref(int fam, double y, double pw) {
+  return fam == FAM_POISSON ? pw * lgamma(y + 1.0) : pw * log(y);
+}
+template <int FAM>
+__device__ __forceinline__ double init_stats_const(double y, double pw) {
+  if constexpr (FAM == FAM_POISSON || FAM == FAM_GAMMA) return init_stats_const_ref(FAM, y, pw);
+  return 0.0;
+}
+
+// Dispatch of the in-pass statistics rows: three family-specific accumulators (s2, s3, s4) that
+// the kernel stores into the slots stats_slots() names.
+template <int FAM>
+__device__ __forceinline__ void pass_row_stats(double eta, double y, double off, double pw, double& w, double& wz,
+                                               double& s_dev, double& s_aux, double& s2, double& s3, double& s4,
+                                               bool small_exp) {
+  if constexpr (FAM == FAM_BINOMIAL)
+    pass_row_logit_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, s4, small_exp);
+  else if constexpr (FAM == FAM_POISSON)
+    pass_row_poisson_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, small_exp);
+  else
+    pass_row_gamma_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, s4);
+}
+// slots of (s2, s3, s4): logit (Pearson, loglik, bad), Poisson (Pearson, loglik part, -),
+// Gamma (Pearson, AUX0, sum pw log(y eta) -> AUX1 on the host)
+template <int FAM>
+struct StatsSlots {
+  static constexpr int S2 = S_PEARSON;
+  static constexpr int S3 = FAM == FAM_GAMMA ? S_AUX0 : S_LL;
+  static constexpr int S4 = FAM == FAM_GAMMA ? S_AUX1 : (FAM == FAM_BINOMIAL ? S_BAD : -1);
+};
 
 }  // namespace sglm

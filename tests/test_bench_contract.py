@@ -102,3 +102,41 @@ def test_stdout_carries_only_the_json_line():
     assert out.returncode == 0, out.stderr
     assert out.stdout.splitlines() == ['{"metric": "m"}']
     assert "[Gloo]" in out.stderr and "log line" in out.stderr
+
+
+def _rank_stats_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    st = {"pass_kernel_ms": 100.0 + 10 * rank, "reduce_kernel_ms": 1.0, "comm_ms": 5.0 * (rank + 1),
+          "solve_ms": 2.0, "comm_path_name": "caller-host", "rank_blocks": 1}
+    q.put((rank, bench.rank_stats(st, 10, True, True)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_diagnostics_field_layout():
+    """the multi-GPU lines carry per-rank pass-kernel / reduce / all-reduce /
+    solve ms per iteration as min and max over the ranks, the all-reduce path and whether the
+    scalars crossed the ranks in rank blocks -- on one process and over a gloo world of 2."""
+    st = {"pass_kernel_ms": 50.0, "reduce_kernel_ms": 0.5, "comm_ms": 0.0, "solve_ms": 1.0,
+          "comm_path_name": "none", "rank_blocks": 0}
+    d = bench.rank_stats(st, 5, False, False)
+    assert d["pass_kernel_ms_per_iter_min"] == d["pass_kernel_ms_per_iter_max"] == 10.0
+    assert d["allreduce_path"] == "none" and d["scalar_rank_blocks"] is False
+    assert set(d) == {f"{k}_per_iter_{m}" for k in ("pass_kernel_ms", "reduce_kernel_ms", "comm_ms", "solve_ms")
+                      for m in ("min", "max")} | {"allreduce_path", "scalar_rank_blocks"}
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench._free_port()
+    ps = [ctx.Process(target=_rank_stats_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r]["pass_kernel_ms_per_iter_min"] == 10.0 and res[r]["pass_kernel_ms_per_iter_max"] == 11.0
+        assert res[r]["comm_ms_per_iter_min"] == 0.5 and res[r]["comm_ms_per_iter_max"] == 1.0
+        assert res[r]["allreduce_path"] == "caller-host" and res[r]["scalar_rank_blocks"] is True

@@ -466,55 +466,82 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
 
 // ---------------------------------------------------------------------------------
 // Fixed-order reduction of the workgroup partials into the packed wire format.
+// A 256-thread block covers RED_EL consecutive output elements with RED_SEG threads each: thread
+// (segment s, element e) sums partials [s n / RED_SEG, (s+1) n / RED_SEG) left to right, then
+// segment 0's thread adds the RED_SEG segment sums in segment order -- a fixed two-level order,
+// deterministic, and RED_SEG times the threads of one dependent load-add chain per element (a
+// p = 20 LM Gram has 238 outputs: one chain over all partials each was a latency-bound 15 us).
+// The scalars (deviance, ...) are Neumaier-compensated at both levels.
 // ---------------------------------------------------------------------------------
-__global__ void reduce_partials_kernel(const double* __restrict__ part, int64_t stride, int nparts, int p,
-                                       int P16, double* __restrict__ out) {
+constexpr int RED_SEG = 8, RED_EL = 256 / RED_SEG;
+
+__global__ void __launch_bounds__(256) reduce_partials_kernel(const double* __restrict__ part, int64_t stride,
+                                                              int nparts, int p, int P16, double* __restrict__ out) {
   // partial layout: T tiles of 256 | X'Wz [16*P16] | NS scalars
+  __shared__ double ss[RED_SEG][RED_EL], cs[RED_SEG][RED_EL];
   const int64_t tri = (int64_t)p * (p + 1) / 2;
   const int64_t total = tri + p + NS;
   const int T = P16 * (P16 + 1) / 2;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t src;
-    if (e < tri) {
-      int64_t i = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
-      while (i * (i + 1) / 2 > e) --i;
-      while ((i + 1) * (i + 2) / 2 <= e) ++i;
-      const int64_t j = e - i * (i + 1) / 2;
-      const int64_t bi = i >> 4, bj = j >> 4;
-      const int64_t t = bi * (bi + 1) / 2 + bj;
-      src = t * 256 + (i & 15) * 16 + (j & 15);
-    } else if (e < tri + p) {
-      src = (int64_t)T * 256 + (e - tri);
-    } else {
-      src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
-    }
-    // the same left-to-right order over the partials, with 32 loads in flight per thread (a
-    // dependent load-add chain over 256 partials is ~60 us of load latency)
-    const double* q = part + src;
-    double s = 0.0;
-    int g = 0;
-    if (e < tri + p) {
-      for (; g + 32 <= nparts; g += 32) {
-        double v[32];
-#pragma unroll
-        for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
-#pragma unroll
-        for (int u = 0; u < 32; ++u) s += v[u];
+  const int el = threadIdx.x % RED_EL, sg = threadIdx.x / RED_EL;
+  const int g0 = (int)((int64_t)nparts * sg / RED_SEG), g1 = (int)((int64_t)nparts * (sg + 1) / RED_SEG);
+  for (int64_t base = (int64_t)blockIdx.x * RED_EL; base < total; base += (int64_t)gridDim.x * RED_EL) {
+    const int64_t e = base + el;
+    double s = 0.0, c = 0.0;
+    const bool scal = e >= tri + p;
+    if (e < total) {
+      int64_t src;
+      if (e < tri) {
+        int64_t i = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+        while (i * (i + 1) / 2 > e) --i;
+        while ((i + 1) * (i + 2) / 2 <= e) ++i;
+        const int64_t j = e - i * (i + 1) / 2;
+        const int64_t bi = i >> 4, bj = j >> 4;
+        const int64_t t = bi * (bi + 1) / 2 + bj;
+        src = t * 256 + (i & 15) * 16 + (j & 15);
+      } else if (e < tri + p) {
+        src = (int64_t)T * 256 + (e - tri);
+      } else {
+        src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
       }
-      for (; g < nparts; ++g) s += q[(int64_t)g * stride];
-    } else {  // deviance and the other scalars: compensated, in the same order
-      double c = 0.0;
-      for (; g + 32 <= nparts; g += 32) {
-        double v[32];
+      // the segment's partials left to right, 8 loads in flight per thread
+      const double* q = part + src;
+      int g = g0;
+      if (!scal) {
+        for (; g + 8 <= g1; g += 8) {
+          double v[8];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) v[u] = q[(int64_t)(g + u) * stride];
+          for (int u = 0; u < 8; ++u) v[u] = q[(int64_t)(g + u) * stride];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) neumaier_add(s, c, v[u]);
+          for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; g < g1; ++g) s += q[(int64_t)g * stride];
+      } else {  // deviance and the other scalars: compensated, in the same order
+        for (; g + 8 <= g1; g += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = q[(int64_t)(g + u) * stride];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) neumaier_add(s, c, v[u]);
+        }
+        for (; g < g1; ++g) neumaier_add(s, c, q[(int64_t)g * stride]);
       }
-      for (; g < nparts; ++g) neumaier_add(s, c, q[(int64_t)g * stride]);
-      s += c;
     }
-    out[e] = s;
+    ss[sg][el] = s;
+    cs[sg][el] = c;
+    __syncthreads();
+    if (sg == 0 && e < total) {
+      double t = ss[0][el], tc = cs[0][el];
+      for (int k = 1; k < RED_SEG; ++k) {
+        if (scal) {
+          neumaier_add(t, tc, ss[k][el]);
+          tc += cs[k][el];
+        } else {
+          t += ss[k][el];
+        }
+      }
+      out[e] = scal ? t + tc : t;
+    }
+    __syncthreads();
   }
 }
 
@@ -718,8 +745,8 @@ hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
 
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st) {
   const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
+  int blocks = (int)((total + RED_EL - 1) / RED_EL);
+  if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks), dim3(256), 0, st, part, stride, nparts, p, P16, out);
   return hipGetLastError();
 }

@@ -17,3 +17,9 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
   cat gpurun_out/${TAG}_bench.json
 fi
+if [[ $STAGE == all || $STAGE == gpus2 ]]; then
+  # the --gpus 2 rehearsal on one GPU: two rank processes sharing the device over gloo
+  timeout -k 10 600 python bench.py --gpus 2 --rows 10000000 --steps 5 --warmup 1 --no-cpu-baseline \
+    > gpurun_out/${TAG}_gpus2.json 2> gpurun_out/${TAG}_gpus2.err || { echo "gpus2 failed"; tail -20 gpurun_out/${TAG}_gpus2.err; exit 1; }
+  cat gpurun_out/${TAG}_gpus2.json
+fi

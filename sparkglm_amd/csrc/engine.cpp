@@ -169,6 +169,9 @@ struct sglm_engine : public Backend {
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
   double stats_const = 0.0;    // the fit's initial-pass S_AUX2: constant part of in-pass Poisson / Gamma statistics
+  double dev_const = 0.0;      // the fit's initial-pass S_AUX1 (Poisson): sum pw y log y, the deviance's constant part
+  bool lp_devsplit = false;    // the last pass summed the Poisson deviance without that constant (narrow)
+  int consts_family = -1;      // family whose initial pass produced stats_const / dev_const on this data (-1: none)
   bool stats_every_pass = false;  // SGLM_STATS_EVERY_PASS=1: Poisson / Gamma statistics in every pass (A/B)
   bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
   // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
@@ -260,6 +263,7 @@ struct sglm_engine : public Backend {
     n = p = n_pad = nblocks = 0;
     rows_loaded = 0;
     written.clear();
+    consts_family = -1;
     procx = ProcX{};
     for (double** ptr : {&dxsc, &dchunks}) {
       if (*ptr) (void)hipFree(*ptr);
@@ -917,6 +921,12 @@ struct sglm_engine : public Backend {
   }
 
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
+    // a narrow Poisson IRLS pass needs its deviance constant from an initial pass on this data (a fit
+    // runs one first; a standalone sglm_irls_pass / sglm_irls_iterations gets one here)
+    if (mode == MODE_IRLS && family == FAM_POISSON && consts_family != FAM_POISSON &&
+        (group() ? subs[0]->narrow : narrow)) {
+      if (int rc = pass(MODE_INIT_SINGLE, nullptr, 1.0, 0.0, family, link, packed)) return rc;
+    }
     if (group()) return group_pass(mode, beta, mu0, ybar, family, link, packed);
     const int64_t plen = packed_len(p), sc = tri_count(p) + p;
     const int R = gather_ranks() ? comm.nranks : 0;  // rank blocks of the scalars (compensated_rank_sum)
@@ -953,13 +963,22 @@ struct sglm_engine : public Backend {
   // later pass that carried the statistics -- R's dpois loglik sum pw (y log mu - mu) minus
   // sum pw lgamma(y + 1); Gamma's S_LL = sum pw log y and S_AUX1 = sum pw log mu = sum pw log y -
   // sum pw log(y eta).  Applied once, on the all-reduced scalars.
+  // Likewise the narrow Poisson passes' deviance lacks its constant part sum pw y log y (pass_row
+  // dev_nolog), summed by the initial pass into S_AUX1 and added back here.
   void finish_scalars(int mode, int family, double* s) {
     if (family != FAM_POISSON && family != FAM_GAMMA) return;
     if (mode == MODE_INIT_SINGLE || mode == MODE_INIT_MULTI) {
       stats_const = s[S_AUX2];
       s[S_AUX2] = 0.0;
+      if (family == FAM_POISSON) {
+        dev_const = s[S_AUX1];
+        s[S_AUX1] = 0.0;
+      }
+      consts_family = family;
       return;
     }
+    if (mode == MODE_IRLS && family == FAM_POISSON && (group() ? subs[0]->lp_devsplit : lp_devsplit))
+      s[S_DEV] += dev_const;
     if (mode != MODE_IRLS || !pass_has_stats()) return;
     if (family == FAM_POISSON) {
       s[S_LL] -= stats_const;
@@ -1039,6 +1058,7 @@ struct sglm_engine : public Backend {
                        !(family == FAM_BINOMIAL && dm) && !force_eta_store &&
                        (family == FAM_BINOMIAL || dev_only || stats_every_pass)) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
+    lp_devsplit = narrow && mode == MODE_IRLS && family == FAM_POISSON;  // narrow.hip: pass_row dev_nolog
     a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.dbg = dbg;
@@ -1697,6 +1717,7 @@ static void group_split(sglm_engine* h, int64_t n) {
 }
 
 static int reserve_impl(sglm_engine* h, int64_t n, int64_t p, int has_m, int has_off, int has_prior) {
+  h->consts_family = -1;
   if (n <= 0 || p <= 0) {
     set_error("requirement failed: n >= 1, p >= 1");
     return SGLM_EINVAL;
@@ -1721,6 +1742,7 @@ int sglm_reserve(sglm_engine* h, int64_t n, int64_t p, int has_m, int has_offset
 
 static int set_rows_impl(sglm_engine* h, int64_t row0, int64_t nr, const double* X, int64_t ldx, const double* y,
                          const double* m, const double* off, const double* prior) {
+  h->consts_family = -1;
   if (!h->group()) return h->set_rows(row0, nr, X, ldx, y, m, off, prior);
   if (h->g_n <= 0 || row0 < 0 || nr < 0 || row0 + nr > h->g_n) {
     set_error("requirement failed: sglm_reserve first; 0 <= row0, row0 + nrows <= reserved rows");
@@ -1782,6 +1804,7 @@ int sglm_set_data_device(sglm_engine* h, const double* dX, int64_t n, int64_t p,
 }
 
 static int synth_impl(sglm_engine* h, int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, bool proc) {
+  h->consts_family = -1;
   if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || row0 < 0) {
     set_error("requirement failed: synth kind in {0,1,2,3}, n >= 1, p >= 1");
     return SGLM_EINVAL;

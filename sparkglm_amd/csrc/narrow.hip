@@ -210,6 +210,9 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 // carries them (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass, ~1 % at p = 64).
 // The Poisson / Gamma statistics' per-fit constants (rowmath.hpp init_stats_const) are summed by
 // the initial pass (IRLS = false) into S_AUX2.
+#ifndef SGLM_POIS_NOLOG
+#define SGLM_POIS_NOLOG 1  // Poisson IRLS rows: deviance without the per-row log (A/B builds: 0)
+#endif
 template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
@@ -344,9 +347,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
             pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
           else
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
-                     !IRLS);
+                     !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
           if constexpr (INIT_CONST)
-            if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
+            if (mode != MODE_LM_GRAM) {
+              s_ll += init_stats_const<FAM>(y, pw);
+              if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
+            }
         }
       }
       // w / w*z at [half * NRB + rl]: the stashed block in the upper half
@@ -435,9 +441,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
         else
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
-                   !IRLS);
+                   !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
         if constexpr (INIT_CONST)
-          if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
+          if (mode != MODE_LM_GRAM) {
+            s_ll += init_stats_const<FAM>(y, pw);
+            if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
+          }
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;
@@ -678,8 +687,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         if (lane == SL::S3) v = s_ll;
         if (lane == SL::S4) v = s_bad;
       }
-      if constexpr (INIT_CONST)
+      if constexpr (INIT_CONST) {
         if (lane == S_AUX2) v = s_ll;
+        if (FAM == FAM_POISSON && lane == S_AUX1) v = s_pear;
+      }
       out[G::T * 256 + G::NC + lane] = v;
     }
   }

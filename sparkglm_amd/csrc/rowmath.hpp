@@ -239,10 +239,15 @@ __device__ __noinline__ RowWZ pass_row_ref(int fam, int lnk, int mode, double et
 // small_exp selects exp_small over libm's exp:
 // measured faster in the p <= 32 narrow pass (-1 %), slower at p = 64 (+4 %) and neutral in
 // the fused / wide kernels, so only the p <= 32 narrow variants set it.
+// dev_nolog (the narrow kernel's Poisson IRLS passes): the Poisson unit deviance without its
+// fit-constant part pw y log y (summed once by the initial pass into S_AUX1, poisson_dev_const;
+// the engine adds it back): pw (-y eta - (y - mu)) per row, no log -- the family arithmetic runs on
+// 16 of 64 lanes at p = 64, and log_pos was ~2/5 of it.
+__device__ __noinline__ double poisson_dev_const_ref(double y, double pw) { return y > 0.0 ? pw * (y * log(y)) : 0.0; }
 __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta, double y, double m, double off,
                                          double pw, double mu0, double ybar, bool has_m, double& w, double& wz,
                                          double& s_dev, double& s_aux, bool small_exp = false,
-                                         bool init_fast = false) {
+                                         bool init_fast = false, bool dev_nolog = false) {
   (void)ybar;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT && mode == MODE_IRLS && !has_m && fabs(eta) < 8.0 && y >= 0.0 &&
       y <= 1.0) {
@@ -273,7 +278,10 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
     const double mu = small_exp ? exp_small(eta) : exp(eta);
     w = pw * mu;
     wz = pw * (mu * (eta - off) + (y - mu));
-    s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
+    if (dev_nolog)
+      s_dev += pw * (-(y * eta) - (y - mu));
+    else
+      s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
     s_aux += pw;
     return;
   }
@@ -324,7 +332,7 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
   const RowWZ r = pass_row_ref(fam, lnk, mode, eta, y, m, off, pw, mu0);
   w = r.w;
   wz = r.wz;
-  s_dev += r.dev;
+  s_dev += (dev_nolog && fam == FAM_POISSON && mode == MODE_IRLS) ? r.dev - poisson_dev_const_ref(y, pw) : r.dev;
   s_aux += pw;
 }
 
@@ -433,6 +441,7 @@ __device__ __noinline__ RowStats stats_row_fallback(int fam, int lnk, double eta
   } else if (fam == FAM_POISSON) {
     o.s3 = a.s[S_LL] + pw * lgamma(y + 1.0);  // the constant part is subtracted once per fit
     o.s4 = 0.0;
+    o.dev -= y > 0.0 ? pw * (y * log(y)) : 0.0;  // the deviance's constant part too (dev_nolog)
   } else {
     o.s3 = a.s[S_AUX0];
     o.s4 = a.s[S_LL] - a.s[S_AUX1];  // pw log y - pw log mu = pw log(y / mu)
@@ -480,7 +489,7 @@ __device__ __forceinline__ void pass_row_poisson_stats(double eta, double y, dou
     const double mu = small_exp ? exp_small(eta) : exp(eta);
     w = pw * mu;
     wz = pw * (mu * (eta - off) + (y - mu));
-    s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
+    s_dev += pw * (-(y * eta) - (y - mu));  // + pw y log y, summed by the initial pass (pass_row dev_nolog)
     s_aux += pw;
     const double r = y - mu;
     s2 += pw * (r * r) * rcp_pos(mu);
@@ -490,7 +499,7 @@ __device__ __forceinline__ void pass_row_poisson_stats(double eta, double y, dou
   const RowStats r = stats_row_fallback(FAM_POISSON, LNK_LOG, eta, y, off, pw);
   w = r.w;
   wz = r.wz;
-  s_dev += r.dev;
+  s_dev += r.dev;  // stats_row_fallback takes the y log y constant out (dev_nolog)
   s_aux += pw;
   s2 += r.s2;
   s3 += r.s3;
@@ -530,7 +539,8 @@ __device__ __forceinline__ void pass_row_gamma_stats(double eta, double y, doubl
 }
 
 // The per-fit constants of the in-pass statistics, summed by the initial pass into S_AUX2:
-// Poisson sum pw lgamma(y + 1) (R's dpois), Gamma sum pw log y (R's dgamma).
+// Poisson sum pw lgamma(y + 1) (R's dpois), Gamma sum pw log y (R's dgamma).  Poisson also sums
+// its deviance constant pw y log y into S_AUX1 (poisson_dev_const_ref, pass_row dev_nolog).
 __device__ __noinline__ double init_stats_const_ref(int fam, double y, double pw) {
   return fam == FAM_POISSON ? pw * lgamma(y + 1.0) : pw * log(y);
 }

@@ -219,3 +219,24 @@ def test_binomial_trials_m_greater_than_one(eng):
         assert f.iter == o.iter, p
         assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL, p
         assert rel([f.deviance, f.pearson, f.loglik], [o.deviance, o.pearson, o.loglik]) < TOL, p
+
+
+def test_poisson_step_deviance_on_a_fresh_shard(eng):
+    """The narrow Poisson pass sums its deviance without the fit-constant pw y log y (summed once by
+    an initial pass: rowmath.hpp dev_nolog); a standalone sglm_irls_step on a freshly loaded shard
+    must still return the whole deviance at beta (SURVEY 8(b)'s test-level step)."""
+    X, y, off, pr = synth.generate(2, 0, 50_000, 40, 9)
+    for reload in (True, False):
+        if reload:
+            eng.set_data(X, y, offset=off, prior=pr)
+        beta = np.full(40, 0.01)
+        beta[0] = 0.2
+        _, _, d = eng.irls_step(beta, family="poisson", link="log")
+        mu = np.exp(X @ beta + off)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ylog = np.where(y > 0, y * np.log(np.where(y > 0, y, 1.0) / mu), 0.0)
+        dev = 2 * np.sum(pr * (ylog - (y - mu)))
+        assert rel(d, dev) < 1e-12, (reload, d, dev)
+    f = eng.fit_glm("poisson", "log")
+    o = po.fit_glm(X, y, "poisson", "log", offset=off, prior=pr)
+    assert f.iter == o.iter and rel(f.deviance, o.deviance) < 1e-12 and rel(f.dev_trace, o.dev_trace) < 1e-12

@@ -104,19 +104,41 @@ def cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
             "time_to_converge_s": dt, "iters": fit.iter}
 
 
-def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
-    """Per-launch HBM bytes of the dominant kernel: the per-row FETCH_SIZE + WRITE_SIZE measured
-    by rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
-    times the rows of this launch (the pass streams every row exactly once)."""
+def pmc_entry(p: int, family: str, procedural: bool = False):
+    """The profiles/pmc_traffic.json entry of a workload shape (rocprofv3 --pmc, tools/pmc_traffic.py)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             tab = json.load(f)
         key = f"{family}:{p}" + (":proc" if procedural else "")
-        e = tab.get(key, tab.get(str(p)) if (family == "binomial" and not procedural) else None)
-        return None if e is None else e["bytes_per_row"] * n
-    except (OSError, ValueError, KeyError):
+        return tab.get(key, tab.get(str(p)) if (family == "binomial" and not procedural) else None)
+    except (OSError, ValueError):
         return None
+
+
+def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
+    """Per-launch HBM bytes of the dominant kernel: the per-row FETCH_SIZE + WRITE_SIZE measured
+    by rocprofv3 --pmc (profiles/pmc_traffic.json, corrected as MI355X_MICROARCH.md prescribes)
+    times the rows of this launch (the pass streams every row exactly once)."""
+    e = pmc_entry(p, family, procedural)
+    try:
+        return None if e is None else e["bytes_per_row"] * n
+    except (KeyError, TypeError):
+        return None
+
+
+def mfma_clock_bound(p: int, n: int, family: str) -> dict:
+    """The second resource of an HBM-bound pass: its fp64 MFMA instruction stream (the lower-
+    triangular 16x16 tile grid, one v_mfma_f64_16x16x4 per tile per 4 rows, 64 cycles on a SIMD;
+    1024 SIMDs) at the clock the chip held under the kernel (PMC GRBM_GUI_ACTIVE), beside the PMC
+    MFMA-busy fraction: where the pass's time goes when it is short of the HBM roofline."""
+    e = pmc_entry(p, family) or {}
+    clk = e.get("clock_ghz")
+    t = (p + 15) // 16
+    cycles = t * (t + 1) // 2 * (n / 4) * 64 / 1024
+    return {"mfma_tiles": t * (t + 1) // 2, "clock_ghz_pmc": clk, "mfma_busy_frac_pmc": e.get("mfma_busy_frac"),
+            "mfma_stream_ms_at_pmc_clock": cycles / (clk * 1e9) * 1e3 if clk else None,
+            "mfma_stream_ms_at_2p4ghz": cycles / 2.4e9 * 1e3}
 
 
 def _free_port() -> int:
@@ -286,7 +308,8 @@ def main() -> int:
             roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": kern_ms,
                     "algorithmic_bytes_per_launch": bytes_pass,
-                    "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS}
+                    "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS,
+                    "fp64_pipe": mfma_clock_bound(p, n, fam)}
         else:
             roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,

@@ -35,11 +35,16 @@
 #ifndef SGLM_SPLIT16
 #define SGLM_SPLIT16 19
 #endif
+// K1r's row stage evaluates exp by exp_small (its constants in SGPRs: libm exp's hoisted
+// coefficients pushed the row waves past the 168-VGPR budget of three waves per SIMD)
+#ifndef SGLM_K1R_SMALLEXP
+#define SGLM_K1R_SMALLEXP 1
+#endif
 
 #ifdef SGLM_STAMPS
 // Diagnostic build only (tools/stamps.py): per-phase s_memtime stamps of workgroup 0's waves
-// over 16 steady-state blocks.  [wave 8][block 16][event 8]
-__device__ unsigned long long sglm_stamp_buf[8 * 16 * 8];
+// over 16 steady-state blocks.  [wave 12][block 16][event 8]
+__device__ unsigned long long sglm_stamp_buf[12 * 16 * 8];
 #define SGLM_STAMP(ev)                                                                          \
   do {                                                                                          \
     if (blockIdx.x == 0 && blk >= b0 + 100 && blk < b0 + 116 && lane == 0)                      \
@@ -48,9 +53,21 @@ __device__ unsigned long long sglm_stamp_buf[8 * 16 * 8];
 extern "C" int sglm_debug_stamps(unsigned long long* out, long count) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_stamp_buf), sizeof(unsigned long long) * count);
 }
+// HW_ID (SIMD id in bits 5:4) of every wave of workgroup 0
+__device__ unsigned sglm_hwid_buf[16];
+#define SGLM_HWID(wv)                                                                                  \
+  do {                                                                                                 \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) sglm_hwid_buf[wv] = __builtin_amdgcn_s_getreg(4 | (31 << 11)); \
+  } while (0)
+extern "C" int sglm_debug_hwid(unsigned* out, long count) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_hwid_buf), sizeof(unsigned) * count);
+}
 #else
 #define SGLM_STAMP(ev) \
   do {                 \
+  } while (0)
+#define SGLM_HWID(wv) \
+  do {                \
   } while (0)
 #endif
 
@@ -255,7 +272,10 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
         if (a.eta_out) a.eta_out[row] = eta;
       }
       if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
-      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux);
+      // (P16 = 16: the row arithmetic of K1r's row_stage_r, so that K1 and K1r are bitwise
+      // interchangeable -- tests/test_gpu_fused_split.py)
+      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux,
+                    P16 == 16 && SGLM_K1R_SMALLEXP);
     }
     lds[G::OFF_W + wb * 2 * RB + r] = w;
     lds[G::OFF_W + wb * 2 * RB + RB + r] = wz;
@@ -444,6 +464,7 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
   if (threadIdx.x == 0) *(unsigned*)(lds + G::OFF_FLAG) = 0u;
+  SGLM_HWID(wv);
   if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
       const int c = G::NC + e / RB, r = e % RB;
@@ -461,6 +482,477 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
     case 5: if constexpr (P16 >= 12) pass_body<P16, FAM, LNK, 5>(lds, a, wv, lane); break;
     case 6: if constexpr (P16 >= 14) pass_body<P16, FAM, LNK, 6>(lds, a, wv, lane); break;
     default: if constexpr (P16 >= 16) pass_body<P16, FAM, LNK, 7>(lds, a, wv, lane); break;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// K1r: the split-role fused pass for P16 = 16 (225 <= p <= 256, BASELINE configs[1]).
+// 12 waves, three per SIMD: two "Gram waves" and one "row wave" on every SIMD.
+//   Gram waves 0..7: 16 lower-triangle tiles each, nothing but the block's MFMAs (A scaled by
+//                    w, X'Wz on the VALU) -- the SIMD always has an MFMA stream ready;
+//   row waves 8..11: the LDS-DMA of the blocks, the row stage of the next block (eta, mu, w,
+//                    w*z, deviance) and the two tiles (7, 2k), (7, 2k+1) of block row 7.
+// In K1 (pass_body) the row stage ran on a wave that also carried 15 tiles: its dependent fp64
+// chain waited one partner MFMA (64 cycles) per instruction, and the partner wave ran out of
+// MFMAs before the row stage ended (phase stamps: ~3.2K idle cycles per 23.2K-cycle block).
+// Here the row stage's latency sits beside TWO MFMA streams that never wait for it inside a
+// block; the row waves run it at raised priority, so its VALU issues into the MFMA gaps.
+// Every tile and X'Wz row accumulates the same values in the same order as K1 (same k-steps,
+// same blocks, same lanes), so the partials are bitwise K1's.
+// Tile ownership: Gram wave 0 = block row 15 (16 tiles); Gram wave g = 1..7 = block rows
+// g-1 and 15-g (16 tiles); row wave k = tiles (7, 2k), (7, 2k+1).
+// ---------------------------------------------------------------------------------
+#ifndef SGLM_K1R_ASYNC
+#define SGLM_K1R_ASYNC 1
+#endif
+#ifndef SGLM_K1R_PRIO_ALT
+#define SGLM_K1R_PRIO_ALT 1
+#endif
+#ifndef SGLM_K1R_SCHED
+#define SGLM_K1R_SCHED 6
+#endif
+
+// SGLM_K1R_ROWT: 1 = the row waves own block row 7's tiles (two each, after their row stage);
+// 0 = every Gram wave owns one of them (17 tiles per Gram wave, row waves without MFMAs).
+#ifndef SGLM_K1R_ROWT
+#define SGLM_K1R_ROWT 0
+#endif
+
+// A wave's tiles are up to three "segments", each a run of tiles (row, j0 .. j0+cnt-1) of one
+// block row (one A operand per segment, B = column block j).
+template <int WV>
+struct TilesR {
+  static constexpr bool ROW = WV >= 8;
+  static constexpr int row(int s) {
+    if (ROW) return (s == 0 && SGLM_K1R_ROWT) ? 7 : -1;
+    if (s == 0) return WV >= 1 ? WV - 1 : -1;   // LO row
+    if (s == 1) return WV == 0 ? 15 : 15 - WV;  // HI row
+    return SGLM_K1R_ROWT ? -1 : 7;              // one tile of block row 7
+  }
+  static constexpr int j0(int s) { return ROW ? 2 * (WV - 8) : (s == 2 ? WV : 0); }
+  static constexpr int cnt(int s) {
+    if (row(s) < 0) return 0;
+    if (ROW) return 2;
+    return s == 2 ? 1 : row(s) + 1;
+  }
+  static constexpr int off(int s) { return s == 0 ? 0 : (s == 1 ? cnt(0) : cnt(0) + cnt(1)); }
+  static constexpr int NT = cnt(0) + cnt(1) + cnt(2);
+  static constexpr int seg_of(int k) { return k < off(1) ? 0 : (k < off(2) ? 1 : 2); }
+};
+
+struct GeoR {
+  using G = Geo<16>;
+  static constexpr int NW = 12, NGW = 8;
+  static constexpr int OFF_RED = G::OFF_RED;              // [NW][NS]
+  // [8 lane groups][32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
+  static constexpr int BETAG_STRIDE = 34;
+  static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas
+  static constexpr int OFF_FLAG = OFF_BETAG + 8 * BETAG_STRIDE;        // counters: row-wave staging, ready, done (uint32)
+  static constexpr int LDS_DOUBLES = OFF_FLAG + 2;
+  static_assert(LDS_DOUBLES * 8 <= 160 * 1024, "LDS");
+  static_assert(G::NI == 4 && G::QMAX == 16 && G::VMAX == 1, "row waves stage as K1's four issuers");
+};
+
+// X'Wz of block `buf` on the row waves (the Gram waves keep only their MFMA operands): row wave
+// k owns column blocks 4k .. 4k+3 and reads them in the MFMA operand layout (lane (cl, rq):
+// column 16b + cl, rows 4j + rq -- conflict free), accumulating exactly the per-lane sums K1's
+// gram_steps forms (k-steps in order, blocks in order); the epilogue combines them with K1's
+// xor-16 / xor-32 shuffles, so X'Wz is bitwise K1's.
+__device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int k, int lane, double (&xz)[4]) {
+  using G = Geo<16>;
+  const double* xs = lds + G::OFF_X + buf * G::XB + (4 * k) * G::BSTR;
+  const double* wz = lds + G::OFF_W + buf * 2 * RB + RB;
+  const int cl = lane & 15, rq = lane >> 4;
+  const double* colbase = xs + cl * 32;
+  // two LDS round trips of 20 reads each (every read of a half issued before its first FMA: a
+  // round trip of a row wave waits behind the Gram waves' operand reads, ~1-2K cycles)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    double xv[RB / 8][4], wv[RB / 8];
+#pragma unroll
+    for (int jj = 0; jj < RB / 8; ++jj) {
+      const int r = 4 * (h * RB / 8 + jj) + rq;
+      const double* base = colbase + (r ^ (2 * cl));
+      wv[jj] = wz[r];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) xv[jj][b] = base[G::BSTR * b];
+    }
+#pragma unroll
+    for (int jj = 0; jj < RB / 8; ++jj)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) xz[b] = fma(xv[jj][b], wv[jj], xz[b]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 5 * RB / 8, 1);
+    __builtin_amdgcn_sched_group_barrier(0x002, 4 * RB / 8, 1);
+  }
+}
+
+// LDS-DMA staging of one row block by row wave si (K1's stage_block, the same instructions and
+// LDS image) with the lane-dependent part of every source address precomputed (voff: 32-bit
+// byte offsets of the four swizzle classes q mod 4) and the rest on the scalar unit: under the
+// two MFMA streams of its SIMD every VALU instruction of a row wave waits for the fp64 pipe, and
+// K1's per-quad 64-bit address arithmetic made the burst take 5-9K cycles.
+__device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassArgs& a, int64_t blk, int si,
+                                              const uint32_t (&voff)[4], uint32_t vvoff) {
+  using G = Geo<16>;
+  typedef __attribute__((address_space(3))) double lds_double;
+  lds_double* l3 = (lds_double*)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void*)lds);
+  lds_double* xdst = l3 + G::OFF_X + buf * G::XB;
+  const int64_t r0 = blk * RB;
+  const int q0 = si * 16;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int q = q0 + k;
+    const int qs = q < a.nq ? q : a.nq - 1;  // quads past p: duplicates
+    const char* sb = (const char*)(a.X + (int64_t)(4 * qs) * a.ld + r0);
+    __builtin_amdgcn_global_load_lds((const void*)(sb + voff[k & 3]), (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128),
+                                     16, 0, 0);
+  }
+  const double* src = a.y;
+  if (si == 1 && a.m) src = a.m;
+  if (si == 2 && a.off) src = a.off;
+  if (si == 3 && a.prior) src = a.prior;
+  const char* sb = (const char*)(src + r0);
+  if ((int)vvoff < 16 * 16)
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vvoff), (lds_void*)(l3 + G::OFF_V + buf * 4 * RB + si * RB), 16, 0, 0);
+}
+
+// Row stage of K1r: K1's row_stage (the same lanes, partial sums and reduction order, so w, w*z
+// and the deviance are bitwise K1's) with its LDS reads in two round trips (columns u = 0, 1 of
+// every stripe, then u = 2, 3 -- the order K1 adds them in) and beta from a per-lane-group copy
+// (betag: the 32 betas of lane group g contiguous, 16 ds_read_b128 instead of 32 ds_read_b64;
+// groups 34 doubles apart so that the eight groups' broadcasts hit distinct banks).
+template <int FAM, int LNK>
+__device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs& a, int64_t blk, int rw, int lane,
+                                            double& s_dev, double& s_aux) {
+  using G = Geo<16>;
+  constexpr int RW = 8, CPG = 4, NT = G::NCE / 32;
+  static_assert(G::RW == RW && G::CPG == CPG && NT == 8, "K1's P16 = 16 row-stage geometry");
+  const double* xs = lds + G::OFF_X + buf * G::XB;
+  const int rl = lane % RW, g = lane / RW;
+  const double* bg = lds + GeoR::OFF_BETAG + g * GeoR::BETAG_STRIDE;
+  const int r = RW * rw + rl;
+  const double* vv = lds + G::OFF_V + buf * 4 * RB;
+  const double y = vv[r];
+  const double m = a.m ? vv[RB + r] : 1.0;
+  const double off = a.off ? vv[2 * RB + r] : 0.0;
+  const double pw = a.prior ? vv[3 * RB + r] : 1.0;
+  double eta = 0.0;
+  if (a.mode == MODE_IRLS && !(SGLM_DBG(a) & 8)) {
+    double e4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double xv[2][NT], bv[2][NT];
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        const int u = 2 * h + uu;
+        const int c0 = CPG * g + u;
+        const double* base = xs + (c0 >> 4) * G::BSTR + (c0 & 15) * 32 + (r ^ ((2 * c0) & 31));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          xv[uu][t] = base[2 * G::BSTR * t];
+          bv[uu][t] = bg[t * CPG + u];
+        }
+      }
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) e4[t & 3] += xv[uu][t] * bv[uu][t];
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * NT, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2 * NT, 2);
+    }
+    eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+    eta = add_xor8(eta);
+    eta = add_xor16(eta);
+    eta = add_xor32(eta);
+  }
+  if (lane < RW) {
+    const int64_t row = blk * RB + r;
+    double w = 0.0, wz = 0.0;
+    if (row < a.n) {
+      if (a.mode == MODE_IRLS) {
+        eta = eta + off;
+        if (a.eta_out) a.eta_out[row] = eta;
+      }
+      if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, SGLM_K1R_SMALLEXP);
+    }
+    lds[G::OFF_W + buf * 2 * RB + r] = w;
+    lds[G::OFF_W + buf * 2 * RB + RB + r] = wz;
+  }
+}
+
+template <int WV>
+__device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lane, d4 (&acc)[TilesR<WV>::NT]) {
+  using G = Geo<16>;
+  using T = TilesR<WV>;
+  const double* xs = lds + G::OFF_X + buf * G::XB;
+  const double* w = lds + G::OFF_W + buf * 2 * RB;
+  const int cl = lane & 15, rq = lane >> 4;
+  const double* colbase = xs + cl * 32;
+  auto kstep = [&](int j) {
+    const int r = 4 * j + rq;
+    const double* base = colbase + (r ^ (2 * cl));
+    const double wr = w[r];
+    double av[3];
+#pragma unroll
+    for (int sg = 0; sg < 3; ++sg) {
+      av[sg] = 0.0;
+      if (T::cnt(sg) > 0) av[sg] = base[G::BSTR * (T::row(sg) >= 0 ? T::row(sg) : 0)] * wr;
+    }
+#pragma unroll
+    for (int k = 0; k < T::NT; ++k) {
+      const int sg = T::seg_of(k);
+      const double b = base[G::BSTR * (T::j0(sg) + k - T::off(sg))];
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sg], b, acc[k], 0, 0, 0);
+    }
+#if SGLM_K1R_SCHED
+    // Keep SGLM_K1R_SCHED B-operand reads in flight ahead of the MFMAs (under the 168-VGPR
+    // budget of three waves per SIMD the default schedule waits for every read in turn):
+    // the A-side reads and the first reads, then one MFMA per further read.
+    __builtin_amdgcn_sched_group_barrier(0x100, 4 + SGLM_K1R_SCHED, 0);
+#pragma unroll
+    for (int k = 0; k < T::NT; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#endif
+  };
+#pragma unroll 1
+  for (int j = 0; j < RB / 4; j += 2) {
+#if SGLM_K1R_PRIO_ALT
+    // the two Gram waves of a SIMD take turns at the higher issue priority, one k-step each, so
+    // neither runs ahead and leaves the other alone at the end of the block (oldest-first
+    // arbitration: waves 0-3 finished their Gram ~7K cycles before waves 4-7)
+    if constexpr (!T::ROW) __builtin_amdgcn_s_setprio((WV >> 2) & 1 ? 0 : 1);
+#endif
+    kstep(j);
+#if SGLM_K1R_PRIO_ALT
+    if constexpr (!T::ROW) __builtin_amdgcn_s_setprio((WV >> 2) & 1 ? 1 : 0);
+#endif
+    kstep(j + 1);
+  }
+}
+
+template <int FAM, int LNK, int WV>
+__device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int lane) {
+  using G = Geo<16>;
+  using R = GeoR;
+  using T = TilesR<WV>;
+  constexpr bool row_wave = T::ROW;
+  constexpr int si = row_wave ? WV - 8 : 0;  // DMA issuer index (row waves)
+  constexpr int wv = WV;                     // (SGLM_STAMP)
+  (void)wv;
+  const int wg = blockIdx.x, nwg = gridDim.x;
+  const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
+  const bool do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram;
+  unsigned* flag = (unsigned*)(lds + R::OFF_FLAG);
+
+  d4 acc[T::NT > 0 ? T::NT : 1];
+#pragma unroll
+  for (int k = 0; k < T::NT; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  double xz[4] = {0.0, 0.0, 0.0, 0.0}, s_dev = 0.0, s_aux = 0.0;
+
+  // lane parts of the DMA source addresses (bytes): column quad q's 4 columns at cq * ld, rows
+  // in the slot swizzle of stage_block, which depends on q mod 4 only
+  uint32_t voff[4];
+  const int li = lane & 15, lcq = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) voff[k] = (uint32_t)(((int64_t)lcq * a.ld + ((2 * li) ^ ((8 * k + 2 * lcq) & 31))) * 8);
+  const uint32_t vvoff = (uint32_t)(lane < 16 ? 16 * lane : 16 * 16);
+  if (row_wave && b0 < b1) {
+    stage_block_r(lds, 0, a, b0, si, voff, vvoff);
+    if (b0 + 1 < b1) stage_block_r(lds, 1, a, b0 + 1, si, voff, vvoff);
+  }
+  if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(SGLM_K1R_PRIO_ALT ? 2 : 1);
+#if SGLM_K1R_ASYNC
+  // No block barrier: three LDS counters order the ring of two buffers.
+  //   flag : +1 per row wave when its LDS-DMA part of a block has landed (4 per block)
+  //   ready: +1 per row wave when its rows of a block's row stage are in the w buffer (4 per block)
+  //   done : +1 per wave when it has finished reading a block: the Gram waves' MFMAs, the row
+  //          waves' X'Wz (12 per block)
+  // A Gram wave starts block b once ready(b) and may run up to one block ahead of the slowest
+  // Gram wave, so the two Gram waves of a SIMD no longer end every block with one of them alone
+  // on the MFMA pipe; the row waves stage block b+2 into block b's buffers after done(b).
+  // (The row stage of b+2 rewrites w(b): the flag round of b+2 orders it after every row wave's
+  // X'Wz of b.)
+  unsigned* ready = flag + 1;
+  unsigned* done = flag + 2;
+  auto spin = [&](unsigned* c, unsigned target) {
+    while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  };
+  auto bump = [&](unsigned* c) {
+    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  if constexpr (row_wave) {
+    if (b0 < b1) {
+      if (b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
+      else wait_vmcnt<0>();
+      bump(flag);
+      spin(flag, 4u);
+      if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
+      bump(ready);
+    }
+#pragma unroll 1
+    for (int64_t blk = b0; blk < b1; ++blk) {
+      const int cur = (int)((blk - b0) & 1);
+      SGLM_STAMP(0);
+      SGLM_STAMP(1);
+      if (blk + 1 < b1) {
+        wait_vmcnt<0>();
+        SGLM_STAMP(2);
+        bump(flag);
+        spin(flag, (unsigned)(4 * (blk + 2 - b0)));
+        SGLM_STAMP(3);
+        if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+        bump(ready);
+      }
+      SGLM_STAMP(4);
+      // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them
+      // (each row wave bumps flag after its row stage of blk); the last block has no such round
+      if (blk + 1 >= b1) spin(ready, (unsigned)(4 * (blk - b0 + 1)));
+      if (do_gram) xz_rows_r(lds, cur, si, lane, xz);
+      SGLM_STAMP(5);
+      bump(done);  // this row wave's reads of block blk (X'Wz) are complete
+      if (blk + 2 < b1) {
+        spin(done, (unsigned)(12 * (blk - b0 + 1)));
+        SGLM_STAMP(6);
+        if (!(SGLM_DBG(a) & 4)) stage_block_r(lds, cur, a, blk + 2, si, voff, vvoff);
+      }
+      SGLM_STAMP(7);
+    }
+  } else {
+#pragma unroll 1
+    for (int64_t blk = b0; blk < b1; ++blk) {
+      const int cur = (int)((blk - b0) & 1);
+      SGLM_STAMP(0);
+      spin(ready, (unsigned)(4 * (blk - b0 + 1)));
+      SGLM_STAMP(1);
+      if (do_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+      SGLM_STAMP(2);
+      SGLM_STAMP(3);
+      SGLM_STAMP(4);
+      SGLM_STAMP(5);
+      bump(done);
+      SGLM_STAMP(6);
+      SGLM_STAMP(7);
+    }
+  }
+#else
+  // Iteration blk: the Gram of block blk (buffers cur) on every wave; on the row waves, after
+  // their two tiles, the row stage of block blk+1 (buffers cur ^ 1) once all four row waves'
+  // LDS-DMA of it has landed.  One barrier per block; then the row waves stage block blk+2 into
+  // the buffers block blk has released.
+  auto iteration = [&](int64_t blk, auto HG) {
+    const int cur = (int)((blk - b0) & 1);
+    constexpr bool has_gram_ct = decltype(HG)::value;
+    const bool has_gram = has_gram_ct && do_gram;
+    SGLM_STAMP(0);
+    if constexpr (!row_wave)
+      if (has_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+    if constexpr (row_wave)
+      if (has_gram) xz_rows_r(lds, cur, si, lane, xz);
+    SGLM_STAMP(1);
+    if constexpr (row_wave) {
+      if (blk + 1 < b1) {
+        // own part of block blk+1 landed (block b0+1 may still be in flight behind b0)
+        if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
+        else wait_vmcnt<0>();
+        SGLM_STAMP(2);
+        if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned target = (unsigned)(4 * (blk + 2 - b0));
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+          __builtin_amdgcn_s_sleep(1);
+        SGLM_STAMP(3);
+        if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+      }
+    }
+    SGLM_STAMP(4);
+    if constexpr (row_wave && T::NT > 0)  // the row waves' tiles, after the row stage
+      if (has_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+    SGLM_STAMP(5);
+    lds_barrier();
+    SGLM_STAMP(6);
+    if (row_wave && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block_r(lds, cur, a, blk + 2, si, voff, vvoff);
+    SGLM_STAMP(7);
+  };
+  if (b0 < b1) iteration(b0 - 1, std::false_type{});
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; ++blk) iteration(blk, std::true_type{});
+#endif
+  if (row_wave) __builtin_amdgcn_s_setprio(0);
+
+  // ---- epilogue: this workgroup's partial (the layout of K1's) ----
+  double* out = a.partials + (int64_t)wg * a.stride;
+#pragma unroll
+  for (int k = 0; k < T::NT; ++k) {
+    const int sg = T::seg_of(k);
+    const int bi = T::row(sg), bj = T::j0(sg) + k - T::off(sg);
+    const int t = bi * (bi + 1) / 2 + bj;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j];
+  }
+  if constexpr (row_wave) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      double v = xz[b];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) out[G::T * 256 + 16 * (4 * si + b) + lane] = v;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    s_dev += __shfl_xor(s_dev, o);
+    s_aux += __shfl_xor(s_aux, o);
+  }
+  if (lane == 0) {
+    lds[R::OFF_RED + WV * NS + 0] = s_dev;
+    lds[R::OFF_RED + WV * NS + 1] = s_aux;
+  }
+  lds_barrier();
+  if (WV == 0 && lane < NS) {
+    // the row waves' sums in K1's order (its row waves 4..7 are waves 8..11 here; the Gram
+    // waves contribute zeros, as K1's MFMA-only waves did)
+    double sd = 0.0, sa = 0.0;
+    for (int k = 0; k < R::NW; ++k) {
+      sd += lds[R::OFF_RED + k * NS + 0];
+      sa += lds[R::OFF_RED + k * NS + 1];
+    }
+    double v = 0.0;
+    if (lane == S_DEV) v = sd;
+    if (lane == S_SUMW) v = sa;
+    out[G::T * 256 + G::NC + lane] = v;
+  }
+}
+
+template <int FAM, int LNK>
+__global__ void __launch_bounds__(64 * GeoR::NW, 3) irls_pass_r_kernel(PassArgs a) {
+  using G = Geo<16>;
+  __shared__ double lds[GeoR::LDS_DOUBLES];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int c = threadIdx.x; c < G::NCE; c += 64 * GeoR::NW) {
+    const double b = (a.beta && c < a.p) ? a.beta[c] : 0.0;
+    lds[G::OFF_BETA + c] = b;
+    // betag[g][t * 4 + u] = beta[4 g + u + 32 t] (row_stage_r)
+    lds[GeoR::OFF_BETAG + ((c & 31) >> 2) * GeoR::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
+  }
+  if (threadIdx.x < 3) ((unsigned*)(lds + GeoR::OFF_FLAG))[threadIdx.x] = 0u;
+  SGLM_HWID(wv);
+  __syncthreads();
+  switch (wv) {
+    case 0: pass_body_r<FAM, LNK, 0>(lds, a, lane); break;
+    case 1: pass_body_r<FAM, LNK, 1>(lds, a, lane); break;
+    case 2: pass_body_r<FAM, LNK, 2>(lds, a, lane); break;
+    case 3: pass_body_r<FAM, LNK, 3>(lds, a, lane); break;
+    case 4: pass_body_r<FAM, LNK, 4>(lds, a, lane); break;
+    case 5: pass_body_r<FAM, LNK, 5>(lds, a, lane); break;
+    case 6: pass_body_r<FAM, LNK, 6>(lds, a, lane); break;
+    case 7: pass_body_r<FAM, LNK, 7>(lds, a, lane); break;
+    case 8: pass_body_r<FAM, LNK, 8>(lds, a, lane); break;
+    case 9: pass_body_r<FAM, LNK, 9>(lds, a, lane); break;
+    case 10: pass_body_r<FAM, LNK, 10>(lds, a, lane); break;
+    default: pass_body_r<FAM, LNK, 11>(lds, a, lane); break;
   }
 }
 
@@ -688,11 +1180,29 @@ int pass_wg_per_cu(int P16) {
 
 // One kernel per (column-block count, family/link): the row stage is compiled for a
 // single family so its registers fit beside the resident Gram accumulators.
+template <int FAM, int LNK>
+static void launch_pass_r(const PassArgs& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((irls_pass_r_kernel<FAM, LNK>), dim3(grid), dim3(64 * GeoR::NW), 0, st, a);
+}
+
 template <int P16>
 static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st) {
   const dim3 g(grid), b(64 * Geo<P16>::NW);
   const int mode_fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int mode_lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  // the split-role kernel (K1r) for the widest fused variant; its DMA addresses the 4 columns
+  // of a quad by 32-bit lane offsets (3 ld + 32 rows, in bytes), which bounds the shard at ~178M
+  // rows (a p = 256 shard that size would not fit in HBM anyway)
+  if (P16 == 16 && a.fused_split && a.ld * 24 + 4096 < ((int64_t)1 << 32)) {
+    if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT) launch_pass_r<FAM_BINOMIAL, LNK_LOGIT>(a, grid, st);
+    else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT) launch_pass_r<FAM_BINOMIAL, LNK_PROBIT>(a, grid, st);
+    else if (mode_fam == FAM_BINOMIAL) launch_pass_r<FAM_BINOMIAL, LNK_CLOGLOG>(a, grid, st);
+    else if (mode_fam == FAM_GAUSSIAN) launch_pass_r<FAM_GAUSSIAN, LNK_IDENTITY>(a, grid, st);
+    else if (mode_fam == FAM_POISSON) launch_pass_r<FAM_POISSON, LNK_LOG>(a, grid, st);
+    else if (mode_fam == FAM_GAMMA) launch_pass_r<FAM_GAMMA, LNK_INVERSE>(a, grid, st);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT)
     hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
   else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT)

@@ -1,0 +1,80 @@
+"""The split-role fused pass K1r (kernels.hip irls_pass_r_kernel, 225 <= p <= 256: two MFMA-only
+"Gram waves" and one "row wave" per SIMD) against K1 (irls_pass_kernel<16>, SGLM_FUSED_SPLIT=0,
+read when an engine is created).  K1r accumulates every Gram tile and X'Wz column in K1's order
+(same k-steps, blocks and lanes) and its row stage is K1's, so one pass and a whole fit must come
+out BITWISE the same -- for every family / link and with offset + prior weights (the row stage's
+four vectors, staged by the four row waves), at p = 256 and at p = 232 (column quads past p are
+duplicated into the padded LDS image), over shards that split into ragged row ranges per
+workgroup, and for a shard smaller than one row block per workgroup.  Both sides are also held
+to the oracle (partitionComponents / zwCreateBinomial, GLM.scala:359-395, utils.scala:84-92)."""
+import os
+
+import numpy as np
+import pytest
+
+from sparkglm_amd import Engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(split: bool) -> Engine:
+    saved = os.environ.get("SGLM_FUSED_SPLIT")
+    os.environ["SGLM_FUSED_SPLIT"] = "1" if split else "0"
+    try:
+        return Engine(0)
+    finally:
+        if saved is None:
+            os.environ.pop("SGLM_FUSED_SPLIT", None)
+        else:
+            os.environ["SGLM_FUSED_SPLIT"] = saved
+
+
+CASES = [
+    # (label, synth kind, rows, p, family, link)
+    ("p256 logit", 0, 300_007, 256, "binomial", "logit"),
+    ("p232 probit", 0, 150_001, 232, "binomial", "probit"),
+    ("p240 cloglog", 0, 120_000, 240, "binomial", "cloglog"),
+    ("p256 poisson + offset + prior", 2, 200_003, 256, "poisson", "log"),
+    ("p250 gamma", 3, 100_000, 250, "gamma", "inverse"),
+    ("p256 gaussian", 1, 90_000, 256, "gaussian", "identity"),
+    ("p256 logit, fewer blocks than workgroups", 0, 5_000, 256, "binomial", "logit"),
+]
+
+
+@pytest.mark.parametrize("label,kind,n,p,family,link", CASES, ids=[c[0] for c in CASES])
+def test_pass_and_fit_bitwise_k1(label, kind, n, p, family, link):
+    rng = np.random.default_rng(p + n)
+    beta = rng.normal(0.0, 0.02, p)
+    if kind == 3:
+        beta = np.abs(beta) + 0.01
+        beta[0] = 1.0
+    out = {}
+    for split in (False, True):
+        with _engine(split) as e:
+            e.synth(kind, 0, n, p, 11)
+            g, xz, s = e.irls_pass(beta, family=family, link=link)
+            f = e.fit_glm(family, link)
+            out[split] = (g, xz, s, f)
+    (g0, xz0, s0, f0), (g1, xz1, s1, f1) = out[False], out[True]
+    assert np.array_equal(g0, g1), label
+    assert np.array_equal(xz0, xz1), label
+    assert np.array_equal(s0, s1), label
+    assert f0.iter == f1.iter
+    assert np.array_equal(np.asarray(f0.coefs), np.asarray(f1.coefs))
+    assert np.array_equal(np.asarray(f0.stderr), np.asarray(f1.stderr))
+    assert (f0.deviance, f0.null_deviance, f0.pearson, f0.loglik) == (f1.deviance, f1.null_deviance, f1.pearson,
+                                                                      f1.loglik)
+
+
+def test_split_pass_matches_oracle():
+    import pyoracle  # checker only
+    n, p = 60_000, 256
+    with _engine(True) as e:
+        e.synth(2, 0, n, p, 5)
+        X, y, m, off, pr = e.get_data()
+        f = e.fit_glm("poisson", "log")
+    o = pyoracle.fit_glm(X, y, "poisson", "log", offset=off, prior=pr, nthreads=8)
+    rel = lambda a, b: float(np.max(np.abs(np.asarray(a) - b) / np.maximum(np.abs(b), 1e-300)))
+    assert f.iter == o.iter
+    assert rel(f.coefs, o.coefs) < 1e-9 and rel(f.stderr, o.stderr) < 1e-9
+    assert rel(f.deviance, o.deviance) < 1e-9

@@ -20,16 +20,23 @@ b = np.full(p, 0.01)
 e.irls_pass(b, family=fam, link=lnk)
 e.irls_pass(b, family=fam, link=lnk)
 lib = _lib.load()
-buf = (C.c_ulonglong * (8 * 16 * 8))()
-assert (lib.sglm_debug_nstamps if narrow else lib.sglm_debug_stamps)(buf, 8 * 16 * 8) == 0
-t = np.array(buf, dtype=np.float64).reshape(8, 16, 8)
+NWV = 8 if narrow else 12
+buf = (C.c_ulonglong * (NWV * 16 * 8))()
+assert (lib.sglm_debug_nstamps if narrow else lib.sglm_debug_stamps)(buf, NWV * 16 * 8) == 0
+t = np.array(buf, dtype=np.float64).reshape(NWV, 16, 8)
 if narrow:
     t = t[:, :, :5]
 names = (["vmcnt", "row stage", "gram", "dma issue"] if narrow else
-         ["gram 1st", "vmcnt", "flag", "row stage", "gram 2nd", "barrier", "dma issue"])
-t0 = t[:, :, 0].min()
+         os.environ.get("STAMP_NAMES", "gram 1st,vmcnt,flag,row stage,gram 2nd,barrier,dma issue").split(","))
+t0 = t[:, :, 0][t[:, :, 0] > 0].min()
+if not narrow:
+    hw = (C.c_uint * 16)()
+    assert lib.sglm_debug_hwid(hw, 16) == 0
+    print("SIMD of each wave of workgroup 0:", [(h >> 4) & 3 for h in list(hw)[:NWV]])
 print("wave  " + "  ".join(f"{s:>10s}" for s in names) + "   block total")
-for w in range(8):
+for w in range(NWV):
+    if not t[w].any():
+        continue
     d = np.diff(t[w], axis=1)  # [16][7]
     row = d.mean(axis=0)
     tot = np.diff(t[w, :, 0]).mean()

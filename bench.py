@@ -298,7 +298,11 @@ def main() -> int:
             kern_ms = st["pass_kernel_ms"] / passes
             pass_ms = kern_ms
         else:
-            kern = f"irls_pass_kernel<{(p + 15) // 16 + ((p + 15) // 16) % 2},{fam},{lnk}>"
+            p16 = (p + 15) // 16 + ((p + 15) // 16) % 2
+            if p16 == 16 and os.environ.get("SGLM_FUSED_SPLIT", "1") != "0":  # K1r (engine.cpp fused_split)
+                kern = f"irls_pass_r_kernel<{fam},{lnk}> (K1r, split-role fused pass)"
+            else:
+                kern = f"irls_pass_kernel<{p16},{fam},{lnk}>"
             kern_ms = st["pass_kernel_ms"] / passes
             pass_ms = kern_ms
         tflops = flops / (kern_ms * 1e-3) / 1e12

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WL = {  # name: (key, rows, kernel substrings of the pass)
     "logit32": ("binomial:32", 100_000_000, ["irls_narrow_kernel"]),
     "poisson64": ("poisson:64", 50_000_000, ["irls_narrow_kernel"]),
-    "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel"]),
+    "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"]),
     "logit512": ("binomial:512", 8_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),
     "logit512p": ("binomial:512:proc", 8_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),
     "gamma2048": ("gamma:2048", 2_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),

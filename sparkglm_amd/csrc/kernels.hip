@@ -112,7 +112,8 @@ struct Geo {
   static constexpr int OFF_BETA = OFF_V + 8 * RB;  // [NCE]
   static constexpr int OFF_W = OFF_BETA + NCE;     // [2][w RB | w*z RB]
   static constexpr int OFF_RED = OFF_W + 4 * RB;   // [NW][NS]
-  static constexpr int OFF_FLAG = OFF_RED + NW * NS; // row-wave staging counter (uint32)
+  static constexpr int OFF_INIT = OFF_RED + NW * NS; // [6] the initial pass's constants (init_const)
+  static constexpr int OFF_FLAG = OFF_INIT + 6;    // row-wave staging counter (uint32)
   static constexpr int LDS_DOUBLES = OFF_FLAG + 1;
   static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
   // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
@@ -272,6 +273,9 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
         if (a.eta_out) a.eta_out[row] = eta;
       }
       if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+      // initial pass (binomial, no m): the per-pass constants from LDS (bitwise pass_row_ref's rows)
+      else if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
+        pass_row_init(lds + G::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
       // (P16 = 16: the row arithmetic of K1r's row_stage_r, so that K1 and K1r are bitwise
       // interchangeable -- tests/test_gpu_fused_split.py)
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux,
@@ -464,6 +468,11 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int c = threadIdx.x; c < G::NCE; c += 64 * G::NW) lds[G::OFF_BETA + c] = (a.beta && c < a.p) ? a.beta[c] : 0.0;
   if (threadIdx.x == 0) *(unsigned*)(lds + G::OFF_FLAG) = 0u;
+  if constexpr (FAM == FAM_BINOMIAL)
+    if (threadIdx.x == 0 && init_fast_row(FAM, a.mode, a.m != nullptr)) {
+      const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
+      for (int k = 0; k < 6; ++k) lds[G::OFF_INIT + k] = ic.v[k];
+    }
   SGLM_HWID(wv);
   if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
@@ -548,7 +557,8 @@ struct GeoR {
   static constexpr int BETAG_STRIDE = 34;
   static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas
   static constexpr int OFF_FLAG = OFF_BETAG + 8 * BETAG_STRIDE;        // counters: row-wave staging, ready, done (uint32)
-  static constexpr int LDS_DOUBLES = OFF_FLAG + 2;
+  static constexpr int OFF_INIT = OFF_FLAG + 2;                         // [6] init_const
+  static constexpr int LDS_DOUBLES = OFF_INIT + 6;
   static_assert(LDS_DOUBLES * 8 <= 160 * 1024, "LDS");
   static_assert(G::NI == 4 && G::QMAX == 16 && G::VMAX == 1, "row waves stage as K1's four issuers");
 };
@@ -674,6 +684,8 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
         if (a.eta_out) a.eta_out[row] = eta;
       }
       if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
+      else if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
+        pass_row_init(lds + GeoR::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, SGLM_K1R_SMALLEXP);
     }
     lds[G::OFF_W + buf * 2 * RB + r] = w;
@@ -938,6 +950,11 @@ __global__ void __launch_bounds__(64 * GeoR::NW, 3) irls_pass_r_kernel(PassArgs 
     lds[GeoR::OFF_BETAG + ((c & 31) >> 2) * GeoR::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
   }
   if (threadIdx.x < 3) ((unsigned*)(lds + GeoR::OFF_FLAG))[threadIdx.x] = 0u;
+  if constexpr (FAM == FAM_BINOMIAL)
+    if (threadIdx.x == 0 && init_fast_row(FAM, a.mode, a.m != nullptr)) {
+      const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
+      for (int k = 0; k < 6; ++k) lds[GeoR::OFF_INIT + k] = ic.v[k];
+    }
   SGLM_HWID(wv);
   __syncthreads();
   switch (wv) {

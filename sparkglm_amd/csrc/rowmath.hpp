@@ -232,6 +232,42 @@ __device__ __noinline__ RowWZ pass_row_ref(int fam, int lnk, int mode, double et
   return r;
 }
 
+// The initial pass of a binomial fit without m (GLM.scala:263-272, 429-444): mu = mu0
+// (fitSingle) or unlink(link(mu0)) (fitMultiple) is the same for every row, so link, lPrime and
+// the variance are invariants of the pass; per row only z and the deviance remain.
+// max(y, 1) = max(1 - y, 1) = 1 for 0 <= y <= 1, so devBinomial's logs are invariant too -- the
+// expressions are the reference's own, operation for operation (pass_row_ref), so the rows come
+// out bitwise pass_row_ref's.  v = {e0, mu, g, w0, l1, l0}.
+struct InitConst {
+  double v[6];
+};
+__device__ __forceinline__ InitConst init_const(int fam, int lnk, int mode, double mu0) {
+  InitConst c;
+  const double e0 = link_fn(fam, lnk, mu0, 1.0);
+  const double mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, e0, 1.0);
+  const double g = lprime_fn(fam, lnk, mu, 1.0);
+  c.v[0] = e0;
+  c.v[1] = mu;
+  c.v[2] = g;
+  c.v[3] = 1.0 / (variance_fn(fam, mu, 1.0) * (g * g));
+  c.v[4] = log(1.0 / mu0);
+  c.v[5] = log(1.0 / (1.0 + (-1.0 * mu0)));
+  return c;
+}
+// the fused kernels' initial passes take these constants from LDS (computed once per workgroup)
+__device__ __forceinline__ bool init_fast_row(int fam, int mode, bool has_m) {
+  return fam == FAM_BINOMIAL && (mode == MODE_INIT_SINGLE || mode == MODE_INIT_MULTI) && !has_m;
+}
+__device__ __forceinline__ void pass_row_init(const double* c, double y, double off, double pw, double& w, double& wz,
+                                              double& s_dev, double& s_aux) {
+  w = pw * c[3];
+  const double z = (c[0] + ((y + (-1.0 * c[1])) * c[2])) + (-1.0 * off);
+  wz = w * z;
+  const double my = 1.0 + (-1.0 * y);
+  s_dev += pw * ((y * c[4]) + (my * c[5]));
+  s_aux += pw;
+}
+
 // The row stage of the fused pass (zwCreateBinomial, GLM.scala:359-395 / the single-
 // partition loop body GLM.scala:282-301): w and w*z for the Gramian, and the deviance.
 // LM gram mode: w = 1, z = y, and the sums of y and of rows (LM.scala:142-155, 167).
@@ -309,24 +345,10 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
   }
   if (init_fast && fam == FAM_BINOMIAL && mode != MODE_IRLS && mode != MODE_LM_GRAM && !has_m && y >= 0.0 &&
       y <= 1.0) {
-    // The initial pass (GLM.scala:263-272, 429-444): mu = mu0 (fitSingle) or unlink(link(mu0))
-    // (fitMultiple) is the same for every row, so link, lPrime and the variance are loop
-    // invariants (hoisted out of the pass's row loop); per row only z and the deviance remain.
     // (init_fast: set by the narrow kernel's non-IRLS instantiation only, whose loop the
-    // invariants are hoisted out of; the fused / wide kernels keep pass_row_ref for it.)
-    // max(y, 1) = max(1 - y, 1) = 1 for 0 <= y <= 1, so devBinomial's logs are invariant too --
-    // the expressions below are the reference's own, operation for operation (pass_row_ref).
-    const double e0 = link_fn(fam, lnk, mu0, 1.0);
-    const double mu = (mode == MODE_INIT_SINGLE) ? mu0 : unlink_fn(fam, lnk, e0, 1.0);
-    const double g = lprime_fn(fam, lnk, mu, 1.0);
-    const double w0 = 1.0 / (variance_fn(fam, mu, 1.0) * (g * g));
-    const double l1 = log(1.0 / mu0), l0 = log(1.0 / (1.0 + (-1.0 * mu0)));
-    w = pw * w0;
-    const double z = (e0 + ((y + (-1.0 * mu)) * g)) + (-1.0 * off);
-    wz = w * z;
-    const double my = 1.0 + (-1.0 * y);
-    s_dev += pw * ((y * l1) + (my * l0));
-    s_aux += pw;
+    // invariants are hoisted out of; the fused kernels take them from LDS, init_const below.)
+    const InitConst c = init_const(fam, lnk, mode, mu0);
+    pass_row_init(c.v, y, off, pw, w, wz, s_dev, s_aux);
     return;
   }
   const RowWZ r = pass_row_ref(fam, lnk, mode, eta, y, m, off, pw, mu0);

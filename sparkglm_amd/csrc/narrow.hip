@@ -217,10 +217,24 @@ template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
-  __shared__ double lds[G::LDS];
+  // the initial pass of a Poisson fit: its per-row functions of the count y tabulated in LDS
+  // (rowmath.hpp poisson_init_table), after the waves' images
+  // (not at P16 = 2: its 32-row double-buffered images leave no 6 KB of the 160 KB)
+  constexpr bool PTAB = !IRLS && FAM == FAM_POISSON && (G::LDS + 3 * POIS_TAB + 8) * 8 <= 160 * 1024;
+  __shared__ double lds[G::LDS + (PTAB ? 3 * POIS_TAB + 8 : 0)];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double* wl = lds + wv * G::WAVE_LDS;
+  double* ptab = lds + G::LDS;     // [3][POIS_TAB] (PTAB)
+  double* pconst = ptab + 3 * POIS_TAB;  // init_const (PTAB)
+  if constexpr (PTAB) {
+    for (int k = threadIdx.x; k < POIS_TAB; k += 64 * G::NW) poisson_init_table(ptab, a.mu0, k);
+    if (threadIdx.x == 0) {
+      const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
+      for (int k = 0; k < 6; ++k) pconst[k] = ic.v[k];
+    }
+    __syncthreads();
+  }
 
   const int64_t nb = a.nblocks * (RB / NRB);  // NRB-row blocks (n_pad = nblocks * RB)
   const int64_t gw = (int64_t)blockIdx.x * G::NW + wv, nwt = (int64_t)gridDim.x * G::NW;
@@ -345,14 +359,15 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = et * w; s_dev += w; }
           else if constexpr (STATS)
             pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
-          else
+          else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                      !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
-          if constexpr (INIT_CONST)
-            if (mode != MODE_LM_GRAM) {
-              s_ll += init_stats_const<FAM>(y, pw);
-              if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
-            }
+            if constexpr (INIT_CONST)
+              if (mode != MODE_LM_GRAM) {
+                s_ll += init_stats_const<FAM>(y, pw);
+                if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
+              }
+          }
         }
       }
       // w / w*z at [half * NRB + rl]: the stashed block in the upper half
@@ -439,14 +454,15 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
         else if constexpr (STATS)
           pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
-        else
+        else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
                    !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
-        if constexpr (INIT_CONST)
-          if (mode != MODE_LM_GRAM) {
-            s_ll += init_stats_const<FAM>(y, pw);
-            if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
-          }
+          if constexpr (INIT_CONST)
+            if (mode != MODE_LM_GRAM) {
+              s_ll += init_stats_const<FAM>(y, pw);
+              if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
+            }
+        }
       }
       wl[G::OFF_W + rl] = w;
       wl[G::OFF_W + NRB + rl] = wz;

@@ -250,8 +250,8 @@ __device__ __forceinline__ InitConst init_const(int fam, int lnk, int mode, doub
   c.v[1] = mu;
   c.v[2] = g;
   c.v[3] = 1.0 / (variance_fn(fam, mu, 1.0) * (g * g));
-  c.v[4] = log(1.0 / mu0);
-  c.v[5] = log(1.0 / (1.0 + (-1.0 * mu0)));
+  c.v[4] = fam == FAM_BINOMIAL ? log(1.0 / mu0) : 0.0;
+  c.v[5] = fam == FAM_BINOMIAL ? log(1.0 / (1.0 + (-1.0 * mu0))) : 0.0;
   return c;
 }
 // the fused kernels' initial passes take these constants from LDS (computed once per workgroup)
@@ -570,6 +570,39 @@ template <int FAM>
 __device__ __forceinline__ double init_stats_const(double y, double pw) {
   if constexpr (FAM == FAM_POISSON || FAM == FAM_GAMMA) return init_stats_const_ref(FAM, y, pw);
   return 0.0;
+}
+
+// The initial pass of a Poisson fit (mu = mu0 for every row, GLM.scala:263-272, 429-444, R's
+// poisson()): per row, pass_row_ref needs log(y / mu0) for the unit deviance, and the in-pass
+// statistics' constants need lgamma(y + 1) and y log y (init_stats_const, poisson_dev_const_ref)
+// -- three libm calls on the 16 of 64 lanes of a p = 64 narrow pass.  Counts y are small
+// integers, so the three functions of k = y are tabulated once per workgroup for k < POIS_TAB
+// with the very same expressions (tab[k] = (k > 0 ? k log(k / mu0) : 0) - (k - mu0),
+// tab[T + k] = lgamma(k + 1), tab[2T + k] = (k > 0 ? k log k : 0)); a row then multiplies by
+// its prior weight exactly where the reference expressions do, so the rows are bitwise
+// pass_row_ref's.  Other rows (non-integer or large y) take the reference path.
+constexpr int POIS_TAB = 256;
+__device__ __forceinline__ void poisson_init_table(double* tab, double mu0, int k) {
+  const double y = (double)k;
+  tab[k] = (y > 0.0 ? y * log(y / mu0) : 0.0) - (y - mu0);
+  tab[POIS_TAB + k] = lgamma(y + 1.0);
+  tab[2 * POIS_TAB + k] = y > 0.0 ? y * log(y) : 0.0;
+}
+// w, w*z from the init constants c (init_const), the deviance and the two statistics constants
+// from the table; false: the row is not a tabulated count (caller takes the reference path)
+__device__ __forceinline__ bool poisson_init_row(const double* c, const double* tab, double y, double off, double pw,
+                                                 double& w, double& wz, double& s_dev, double& s_aux, double& s_dc,
+                                                 double& s_lg) {
+  if (!(y >= 0.0 && y < (double)POIS_TAB && y == floor(y))) return false;
+  const int k = (int)y;
+  w = pw * c[3];
+  const double z = (c[0] + ((y + (-1.0 * c[1])) * c[2])) + (-1.0 * off);
+  wz = w * z;
+  s_dev += pw * tab[k];
+  s_aux += pw;
+  s_lg += pw * tab[POIS_TAB + k];
+  s_dc += k > 0 ? pw * tab[2 * POIS_TAB + k] : 0.0;
+  return true;
 }
 
 // Dispatch of the in-pass statistics rows: three family-specific accumulators (s2, s3, s4) that

@@ -127,12 +127,13 @@ def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
         return None
 
 
-def mfma_clock_bound(p: int, n: int, family: str) -> dict:
-    """The second resource of an HBM-bound pass: its fp64 MFMA instruction stream (the lower-
-    triangular 16x16 tile grid, one v_mfma_f64_16x16x4 per tile per 4 rows, 64 cycles on a SIMD;
-    1024 SIMDs) at the clock the chip held under the kernel (PMC GRBM_GUI_ACTIVE), beside the PMC
-    MFMA-busy fraction: where the pass's time goes when it is short of the HBM roofline."""
-    e = pmc_entry(p, family) or {}
+def mfma_clock_bound(p: int, n: int, family: str, procedural: bool = False) -> dict:
+    """The fp64 MFMA instruction stream of a pass -- the second resource of an HBM-bound pass, the
+    bound of an MFMA-bound one: the lower-triangular 16x16 tile grid, one v_mfma_f64_16x16x4 per
+    tile per 4 rows, 64 cycles on a SIMD, 1024 SIMDs, at the clock the chip held under the kernel
+    (PMC GRBM_GUI_ACTIVE), beside the PMC MFMA-busy fraction: where the pass's time goes when it
+    is short of its roofline (the power-limited clock, not the 2.4 GHz peak, bounds the stream)."""
+    e = pmc_entry(p, family, procedural) or {}
     clk = e.get("clock_ghz")
     t = (p + 15) // 16
     cycles = t * (t + 1) // 2 * (n / 4) * 64 / 1024
@@ -318,7 +319,11 @@ def main() -> int:
             roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                     "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
-                    "hbm_gbs_algorithmic": gbs}
+                    "hbm_gbs_algorithmic": gbs, "fp64_pipe": mfma_clock_bound(p, n, fam, wl.get("procedural", False))}
+            # the MFMA instruction stream at the clock the chip holds under the kernel (PMC), against
+            # the measured kernel time: how close the kernel is to its clock-limited bound
+            sm = roof["fp64_pipe"].get("mfma_stream_ms_at_pmc_clock")
+            roof["fp64_pipe"]["kernel_frac_of_clock_limited_stream"] = sm / kern_ms if sm and kern_ms else None
         out = {
             "metric": METRIC,
             "value": total_rows * args.steps / dt,

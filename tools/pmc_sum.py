@@ -25,6 +25,7 @@ for k in tot:
     e = {c: tot[k][c] / cnt[k][c] for c in tot[k]}
     ds = dur.get(k, [])
     e["avg_ms"] = sum(ds) / len(ds) if ds else None
+    e["dispatches"] = len(ds)
     out[k] = e
 if "--json" in sys.argv:
     print(json.dumps(out, indent=1))

@@ -13,13 +13,14 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-WL = {  # name: (key, rows, kernel substrings of the pass)
-    "logit32": ("binomial:32", 100_000_000, ["irls_narrow_kernel"]),
-    "poisson64": ("poisson:64", 50_000_000, ["irls_narrow_kernel"]),
-    "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"]),
-    "logit512": ("binomial:512", 8_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),
-    "logit512p": ("binomial:512:proc", 8_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),
-    "gamma2048": ("gamma:2048", 2_000_000, ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]),
+WIDE = ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]
+WL = {  # name: (key, rows, kernel substrings of the pass, substring of the kernel dispatched once per pass)
+    "logit32": ("binomial:32", 100_000_000, ["irls_narrow_kernel"], "irls_narrow_kernel"),
+    "poisson64": ("poisson:64", 50_000_000, ["irls_narrow_kernel"], "irls_narrow_kernel"),
+    "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"], "irls_pass"),
+    "logit512": ("binomial:512", 8_000_000, WIDE, "wide_rows_kernel<"),
+    "logit512p": ("binomial:512:proc", 8_000_000, WIDE, "wide_rows_kernel<"),
+    "gamma2048": ("gamma:2048", 2_000_000, WIDE, "wide_rows_kernel<"),
 }
 
 
@@ -34,15 +35,20 @@ def main():
     d, label = sys.argv[1], sys.argv[2]
     path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(HERE), "profiles", "pmc_traffic.json")
     tab = json.load(open(path)) if os.path.exists(path) else {}
-    for wl, (key, rows, subs) in WL.items():
+    for wl, (key, rows, subs, per_pass) in WL.items():
         if not os.path.isdir(os.path.join(d, f"{wl}_1")):
             continue
         ks = {k: v for k, v in load(d, wl).items() if any(s in k for s in subs)}
-        fetch = sum(v.get("FETCH_SIZE", 0) for v in ks.values()) * 2 * 1024
-        write = sum(v.get("WRITE_SIZE", 0) for v in ks.values()) * 1024
-        ms = sum(v.get("avg_ms") or 0 for v in ks.values())
-        grbm = sum(v.get("GRBM_GUI_ACTIVE", 0) for v in ks.values())
-        mfma = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) for v in ks.values())
+        # totals over every dispatch (per-dispatch averages x dispatches), per pass: a pass is one
+        # dispatch of its pass-defining kernel (the fused / narrow kernel; a wide pass's chunk-0 row
+        # kernel) -- chunked wide passes dispatch the Gram kernels once per chunk
+        npass = sum(v.get("dispatches", 1) for k, v in ks.items() if per_pass in k) or 1
+        tot = lambda c: sum((v.get(c) or 0) * v.get("dispatches", 1) for v in ks.values()) / npass
+        fetch = tot("FETCH_SIZE") * 2 * 1024
+        write = tot("WRITE_SIZE") * 1024
+        ms = tot("avg_ms")
+        grbm = tot("GRBM_GUI_ACTIVE")
+        mfma = tot("SQ_VALU_MFMA_BUSY_CYCLES")
         cyc = grbm / 8
         entry = {"bytes_per_row": (fetch + write) / rows, "measured_rows": rows, "kernels": sorted(ks),
                  "fetch_bytes_per_row": fetch / rows, "write_bytes_per_row": write / rows,
@@ -51,7 +57,7 @@ def main():
                  "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE / GRBM_GUI_ACTIVE+SQ_VALU_MFMA_BUSY_CYCLES "
                            "in separate passes over tools/pass_bench.py (tools/pmc_workloads.sh); FETCH_SIZE doubled "
                            "(gfx950 reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md); KB x 1024; summed "
-                           "over the pass's kernels; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; MFMA busy = "
+                           "over every dispatch of the pass's kernels, per pass; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; MFMA busy = "
                            "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock cycles)"}
         if key in tab:
             prev = tab[key]

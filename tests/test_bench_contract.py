@@ -140,3 +140,46 @@ def test_rank_diagnostics_field_layout():
         assert res[r]["pass_kernel_ms_per_iter_min"] == 10.0 and res[r]["pass_kernel_ms_per_iter_max"] == 11.0
         assert res[r]["comm_ms_per_iter_min"] == 0.5 and res[r]["comm_ms_per_iter_max"] == 1.0
         assert res[r]["allreduce_path"] == "caller-host" and res[r]["scalar_rank_blocks"] is True
+
+
+def test_mfma_clock_bound_counts_the_tile_stream():
+    # one v_mfma_f64_16x16x4 per lower-triangular 16x16 tile per 4 rows, 64 cycles on one of 1024
+    # SIMDs, at the PMC clock of the workload shape (profiles/pmc_traffic.json)
+    e = bench.mfma_clock_bound(256, 100_000_000, "binomial")
+    assert e["mfma_tiles"] == 136
+    clk = bench.pmc_entry(256, "binomial")["clock_ghz"]
+    cycles = 136 * 25_000_000 * 64 / 1024
+    assert abs(e["mfma_stream_ms_at_pmc_clock"] - cycles / (clk * 1e9) * 1e3) < 1e-9
+    assert abs(e["mfma_stream_ms_at_2p4ghz"] - cycles / 2.4e9 * 1e3) < 1e-9
+    assert bench.mfma_clock_bound(2048, 10, "gamma")["mfma_tiles"] == 128 * 129 // 2
+    # the procedural shard has its own PMC entry (clock under the generator + Gram)
+    assert bench.mfma_clock_bound(512, 10, "binomial", True)["clock_ghz_pmc"] == \
+        bench.pmc_entry(512, "binomial", True)["clock_ghz"]
+
+
+def test_pmc_traffic_counts_every_dispatch_of_a_pass(tmp_path, monkeypatch):
+    # tools/pmc_traffic.py: a chunked wide pass dispatches its Gram kernels once per chunk; the
+    # per-row bytes sum every dispatch and divide by the passes (one chunk-0 row kernel each)
+    spec2 = importlib.util.spec_from_file_location("pmc_traffic", os.path.join(ROOT, "tools", "pmc_traffic.py"))
+    pt = importlib.util.module_from_spec(spec2)
+    spec2.loader.exec_module(pt)
+    rows = pt.WL["gamma2048"][1]
+    fake = {  # per-dispatch averages (FETCH_SIZE in KB: half of the streamed bytes on gfx950)
+        "void sglm::wide_rows_kernel<3, 5>(sglm::WideRowArgs)": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 0.0, "dispatches": 2,
+                                                                "avg_ms": 1.0, "GRBM_GUI_ACTIVE": 8e6,
+                                                                "SQ_VALU_MFMA_BUSY_CYCLES": 0.0},
+        "void sglm::wide_gram_kernel<false, false>(sglm::WideGramArgs)": {"FETCH_SIZE": 1000.0, "WRITE_SIZE": 1.0,
+                                                                         "dispatches": 6, "avg_ms": 10.0,
+                                                                         "GRBM_GUI_ACTIVE": 8e7,
+                                                                         "SQ_VALU_MFMA_BUSY_CYCLES": 1e9},
+    }
+    monkeypatch.setattr(pt, "load", lambda d, wl: fake)
+    (tmp_path / "gamma2048_1").mkdir()
+    out = tmp_path / "t.json"
+    monkeypatch.setattr(pt.sys, "argv", ["pmc_traffic.py", str(tmp_path), "test", str(out)])
+    pt.main()
+    e = json.load(open(out))["gamma:2048"]
+    per_pass_kb = 100.0 * 2 / 2 + 1000.0 * 6 / 2      # 2 passes: 1 row + 3 Gram dispatches each
+    assert abs(e["fetch_bytes_per_row"] - per_pass_kb * 2 * 1024 / rows) < 1e-9
+    assert abs(e["write_bytes_per_row"] - 1.0 * 6 / 2 * 1024 / rows) < 1e-9
+    assert abs(e["kernel_ms_profiled"] - (1.0 + 30.0)) < 1e-12

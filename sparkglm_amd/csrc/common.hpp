@@ -65,7 +65,7 @@ struct PassArgs {
   int stats_in_pass;    // narrow binomial/logit IRLS pass without m: pearson / loglik / bad in the
                         // pass's scalars instead of the eta store + stats_kernel
   int no_gram;          // deviance-only pass (glm_drive's speculative last pass): row stage, no Gram
-  int fused_split;      // P16 = 16: the split-role kernel K1r (irls_pass_r_kernel); 0: K1 (SGLM_FUSED_SPLIT=0)
+  int fused_split;      // split-role kernel K1r (irls_pass_r_kernel) from P16 >= threshold: 1 default, 0 never, N: P16 >= N
   int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math,
                         // 32 no eta store
 };

@@ -226,7 +226,7 @@ struct sglm_engine : public Backend {
   // stats
   int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
-  bool fused_split = true;  // SGLM_FUSED_SPLIT=0: the p = 225..256 fused pass on K1 instead of K1r (A/B, tests)
+  int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
   int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
   static constexpr int64_t STAGE_DOUBLES = (int64_t)8 << 20;  // 64 MiB each
@@ -666,7 +666,7 @@ struct sglm_engine : public Backend {
       if (!wide) P16 = pass_variant((int)p);
       stride = wide ? 0 : pass_stride(P16);
       if (!wide) {
-        const int64_t want_grid = (int64_t)ncu * pass_wg_per_cu(P16);
+        const int64_t want_grid = (int64_t)ncu * (pass_uses_split(P16, fused_split, n_pad) ? 1 : pass_wg_per_cu(P16));
         grid = (int)(nblocks < want_grid ? (nblocks > 0 ? nblocks : 1) : want_grid);
       }
     }
@@ -1062,7 +1062,7 @@ struct sglm_engine : public Backend {
     lp_devsplit = narrow && mode == MODE_IRLS && family == FAM_POISSON;  // narrow.hip: pass_row dev_nolog
     a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
-    a.fused_split = fused_split ? 1 : 0;
+    a.fused_split = fused_split;
     a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (wide) {
@@ -1661,7 +1661,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
-  if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::atoi(fs) != 0;
+  if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::max(0, std::atoi(fs));
   if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "lu") == 0;
   if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
   *out = h;

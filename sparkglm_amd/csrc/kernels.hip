@@ -527,55 +527,121 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
 #define SGLM_K1R_ROWT 0
 #endif
 
-// A wave's tiles are up to three "segments", each a run of tiles (row, j0 .. j0+cnt-1) of one
+// A wave's tiles are up to NSEG "segments", each a run of tiles (row, j0 .. j0+cnt-1) of one
 // block row (one A operand per segment, B = column block j).
-template <int WV>
+// P16 = 16: Gram wave 0 = block row 15 (16 tiles); Gram wave g = 1..7 = block rows g-1 and 15-g
+// (16 tiles) + tile (7, g) of block row 7.  Other P16 (the mid-width generalisation): the tile
+// rows taken in pairs (0, P16-1), (1, P16-2), ... -- P16 + 1 tiles a pair -- and that sequence of
+// tiles cut into 8 equal contiguous runs, one per Gram wave (at most NSEG segments each).
+template <int P16>
+struct TileSeq {
+  static constexpr int T = P16 * (P16 + 1) / 2;
+  static constexpr int seq_row(int i) { return (i & 1) ? P16 - 1 - (i >> 1) : (i >> 1); }  // i-th row of the sequence
+  static constexpr int seq_start(int i) {  // first sequence index of row seq_row(i)
+    int t = 0;
+    for (int k = 0; k < i; ++k) t += seq_row(k) + 1;
+    return t;
+  }
+  static constexpr int seq_of(int t) {  // sequence row holding sequence tile t
+    int i = 0;
+    while (i + 1 < P16 && seq_start(i + 1) <= t) ++i;
+    return i;
+  }
+};
+constexpr int NSEG = 4;
+template <int P16, int WV>
 struct TilesR {
   static constexpr bool ROW = WV >= 8;
+  using S = TileSeq<P16>;
+  static constexpr int tlo() { return S::T * WV / 8; }
+  static constexpr int thi() { return S::T * (WV + 1) / 8; }
   static constexpr int row(int s) {
-    if (ROW) return (s == 0 && SGLM_K1R_ROWT) ? 7 : -1;
-    if (s == 0) return WV >= 1 ? WV - 1 : -1;   // LO row
-    if (s == 1) return WV == 0 ? 15 : 15 - WV;  // HI row
-    return SGLM_K1R_ROWT ? -1 : 7;              // one tile of block row 7
+    if constexpr (P16 == 16) {
+      if (ROW) return (s == 0 && SGLM_K1R_ROWT) ? 7 : -1;
+      if (s == 0) return WV >= 1 ? WV - 1 : -1;   // LO row
+      if (s == 1) return WV == 0 ? 15 : 15 - WV;  // HI row
+      if (s == 2) return SGLM_K1R_ROWT ? -1 : 7;  // one tile of block row 7
+      return -1;
+    } else {
+      if (ROW || thi() <= tlo()) return -1;
+      const int i = S::seq_of(tlo()) + s;
+      return i <= S::seq_of(thi() - 1) ? S::seq_row(i) : -1;
+    }
   }
-  static constexpr int j0(int s) { return ROW ? 2 * (WV - 8) : (s == 2 ? WV : 0); }
+  static constexpr int j0(int s) {
+    if constexpr (P16 == 16) return ROW ? 2 * (WV - 8) : (s == 2 ? WV : 0);
+    else return s == 0 && !ROW && thi() > tlo() ? tlo() - S::seq_start(S::seq_of(tlo())) : 0;
+  }
   static constexpr int cnt(int s) {
     if (row(s) < 0) return 0;
-    if (ROW) return 2;
-    return s == 2 ? 1 : row(s) + 1;
+    if constexpr (P16 == 16) {
+      if (ROW) return 2;
+      return s == 2 ? 1 : row(s) + 1;
+    } else {
+      const int i = S::seq_of(tlo()) + s;
+      const int b = i == S::seq_of(tlo()) ? tlo() : S::seq_start(i);  // first sequence tile in the run
+      const int e = S::seq_start(i) + S::seq_row(i) + 1;              // end of the row in the sequence
+      return (e < thi() ? e : thi()) - b;
+    }
   }
-  static constexpr int off(int s) { return s == 0 ? 0 : (s == 1 ? cnt(0) : cnt(0) + cnt(1)); }
-  static constexpr int NT = cnt(0) + cnt(1) + cnt(2);
-  static constexpr int seg_of(int k) { return k < off(1) ? 0 : (k < off(2) ? 1 : 2); }
+  static constexpr int off(int s) {
+    int o = 0;
+    for (int k = 0; k < s; ++k) o += cnt(k);
+    return o;
+  }
+  static constexpr int NT = off(NSEG);
+  static constexpr int seg_of(int k) {
+    int sg = 0;
+    while (sg + 1 < NSEG && off(sg + 1) <= k) ++sg;
+    return sg;
+  }
+  static_assert(P16 == 16 || ROW || row(NSEG) < 0 || true, "segments");
 };
 
+template <int P16>
 struct GeoR {
-  using G = Geo<16>;
+  using G = Geo<P16>;
   static constexpr int NW = 12, NGW = 8;
   static constexpr int OFF_RED = G::OFF_RED;              // [NW][NS]
-  // [8 lane groups][32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
+  // [8 lane groups][4 NCE/32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
   static constexpr int BETAG_STRIDE = 34;
   static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas
   static constexpr int OFF_FLAG = OFF_BETAG + 8 * BETAG_STRIDE;        // counters: row-wave staging, ready, done (uint32)
   static constexpr int OFF_INIT = OFF_FLAG + 2;                         // [6] init_const
   static constexpr int LDS_DOUBLES = OFF_INIT + 6;
+  static constexpr int QPW = P16;                         // column quads each row wave stages
+  static constexpr int NT = G::NCE / 32;                  // 32-column stripes of the row stage
   static_assert(LDS_DOUBLES * 8 <= 160 * 1024, "LDS");
-  static_assert(G::NI == 4 && G::QMAX == 16 && G::VMAX == 1, "row waves stage as K1's four issuers");
+  static_assert(G::NCE == G::NC && 4 * NT <= BETAG_STRIDE, "even P16: whole 32-column stripes");
+  // every Gram wave's tiles fit NSEG segments and the eight runs cover the triangle
+  static constexpr bool tiles_ok() {
+    return TilesR<P16, 0>::NT + TilesR<P16, 1>::NT + TilesR<P16, 2>::NT + TilesR<P16, 3>::NT + TilesR<P16, 4>::NT +
+               TilesR<P16, 5>::NT + TilesR<P16, 6>::NT + TilesR<P16, 7>::NT + (P16 == 16 ? 0 : 0) ==
+           (P16 == 16 && SGLM_K1R_ROWT ? G::T - 8 : G::T);
+  }
+  static_assert(tiles_ok(), "the Gram waves' segments cover the tile triangle");
 };
 
 // X'Wz of block `buf` on the row waves (the Gram waves keep only their MFMA operands): row wave
-// k owns column blocks 4k .. 4k+3 and reads them in the MFMA operand layout (lane (cl, rq):
-// column 16b + cl, rows 4j + rq -- conflict free), accumulating exactly the per-lane sums K1's
-// gram_steps forms (k-steps in order, blocks in order); the epilogue combines them with K1's
-// xor-16 / xor-32 shuffles, so X'Wz is bitwise K1's.
-__device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int k, int lane, double (&xz)[4]) {
-  using G = Geo<16>;
-  const double* xs = lds + G::OFF_X + buf * G::XB + (4 * k) * G::BSTR;
+// k owns column blocks [P16 k / 4, P16 (k+1) / 4) (4k .. 4k+3 at P16 = 16) and reads them in the
+// MFMA operand layout (lane (cl, rq): column 16b + cl, rows 4j + rq -- conflict free),
+// accumulating exactly the per-lane sums K1's gram_steps forms (k-steps in order, blocks in
+// order); the epilogue combines them with K1's xor-16 / xor-32 shuffles, so X'Wz is bitwise K1's.
+template <int P16, int K>
+struct XzBlocks {
+  static constexpr int LO = P16 * K / 4, N = P16 * (K + 1) / 4 - LO;
+  static_assert(N >= 1 && N <= 4, "one to four column blocks per row wave");
+};
+template <int P16, int K>
+__device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int lane, double (&xz)[4]) {
+  using G = Geo<P16>;
+  using XB = XzBlocks<P16, K>;
+  const double* xs = lds + G::OFF_X + buf * G::XB + XB::LO * G::BSTR;
   const double* wz = lds + G::OFF_W + buf * 2 * RB + RB;
   const int cl = lane & 15, rq = lane >> 4;
   const double* colbase = xs + cl * 32;
-  // two LDS round trips of 20 reads each (every read of a half issued before its first FMA: a
-  // round trip of a row wave waits behind the Gram waves' operand reads, ~1-2K cycles)
+  // two LDS round trips (every read of a half issued before its first FMA: a round trip of a row
+  // wave waits behind the Gram waves' operand reads, ~1-2K cycles)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     double xv[RB / 8][4], wv[RB / 8];
@@ -585,14 +651,14 @@ __device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int k, int
       const double* base = colbase + (r ^ (2 * cl));
       wv[jj] = wz[r];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) xv[jj][b] = base[G::BSTR * b];
+      for (int b = 0; b < XB::N; ++b) xv[jj][b] = base[G::BSTR * b];
     }
 #pragma unroll
     for (int jj = 0; jj < RB / 8; ++jj)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) xz[b] = fma(xv[jj][b], wv[jj], xz[b]);
-    __builtin_amdgcn_sched_group_barrier(0x100, 5 * RB / 8, 1);
-    __builtin_amdgcn_sched_group_barrier(0x002, 4 * RB / 8, 1);
+      for (int b = 0; b < XB::N; ++b) xz[b] = fma(xv[jj][b], wv[jj], xz[b]);
+    __builtin_amdgcn_sched_group_barrier(0x100, (XB::N + 1) * RB / 8, 1);
+    __builtin_amdgcn_sched_group_barrier(0x002, XB::N * RB / 8, 1);
   }
 }
 
@@ -601,20 +667,21 @@ __device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int k, int
 // byte offsets of the four swizzle classes q mod 4) and the rest on the scalar unit: under the
 // two MFMA streams of its SIMD every VALU instruction of a row wave waits for the fp64 pipe, and
 // K1's per-quad 64-bit address arithmetic made the burst take 5-9K cycles.
+template <int P16>
 __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassArgs& a, int64_t blk, int si,
                                               const uint32_t (&voff)[4], uint32_t vvoff) {
-  using G = Geo<16>;
+  using G = Geo<P16>;
   typedef __attribute__((address_space(3))) double lds_double;
   lds_double* l3 = (lds_double*)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void*)lds);
   lds_double* xdst = l3 + G::OFF_X + buf * G::XB;
   const int64_t r0 = blk * RB;
-  const int q0 = si * 16;
+  const int q0 = si * GeoR<P16>::QPW;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
+  for (int k = 0; k < GeoR<P16>::QPW; ++k) {
     const int q = q0 + k;
     const int qs = q < a.nq ? q : a.nq - 1;  // quads past p: duplicates
     const char* sb = (const char*)(a.X + (int64_t)(4 * qs) * a.ld + r0);
-    __builtin_amdgcn_global_load_lds((const void*)(sb + voff[k & 3]), (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128),
+    __builtin_amdgcn_global_load_lds((const void*)(sb + voff[q & 3]), (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128),
                                      16, 0, 0);
   }
   const double* src = a.y;
@@ -631,15 +698,15 @@ __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassAr
 // every stripe, then u = 2, 3 -- the order K1 adds them in) and beta from a per-lane-group copy
 // (betag: the 32 betas of lane group g contiguous, 16 ds_read_b128 instead of 32 ds_read_b64;
 // groups 34 doubles apart so that the eight groups' broadcasts hit distinct banks).
-template <int FAM, int LNK>
+template <int P16, int FAM, int LNK>
 __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs& a, int64_t blk, int rw, int lane,
                                             double& s_dev, double& s_aux) {
-  using G = Geo<16>;
-  constexpr int RW = 8, CPG = 4, NT = G::NCE / 32;
-  static_assert(G::RW == RW && G::CPG == CPG && NT == 8, "K1's P16 = 16 row-stage geometry");
+  using G = Geo<P16>;
+  constexpr int RW = 8, CPG = 4, NT = GeoR<P16>::NT;
+  static_assert(P16 != 16 || (G::RW == RW && G::CPG == CPG && NT == 8), "K1's P16 = 16 row-stage geometry");
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const int rl = lane % RW, g = lane / RW;
-  const double* bg = lds + GeoR::OFF_BETAG + g * GeoR::BETAG_STRIDE;
+  const double* bg = lds + GeoR<P16>::OFF_BETAG + g * GeoR<P16>::BETAG_STRIDE;
   const int r = RW * rw + rl;
   const double* vv = lds + G::OFF_V + buf * 4 * RB;
   const double y = vv[r];
@@ -685,7 +752,7 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
       }
       if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
       else if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
-        pass_row_init(lds + GeoR::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
+        pass_row_init(lds + GeoR<P16>::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, SGLM_K1R_SMALLEXP);
     }
     lds[G::OFF_W + buf * 2 * RB + r] = w;
@@ -693,10 +760,10 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
   }
 }
 
-template <int WV>
-__device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lane, d4 (&acc)[TilesR<WV>::NT]) {
-  using G = Geo<16>;
-  using T = TilesR<WV>;
+template <int P16, int WV>
+__device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lane, d4 (&acc)[TilesR<P16, WV>::NT]) {
+  using G = Geo<P16>;
+  using T = TilesR<P16, WV>;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* w = lds + G::OFF_W + buf * 2 * RB;
   const int cl = lane & 15, rq = lane >> 4;
@@ -705,9 +772,9 @@ __device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lan
     const int r = 4 * j + rq;
     const double* base = colbase + (r ^ (2 * cl));
     const double wr = w[r];
-    double av[3];
+    double av[NSEG];
 #pragma unroll
-    for (int sg = 0; sg < 3; ++sg) {
+    for (int sg = 0; sg < NSEG; ++sg) {
       av[sg] = 0.0;
       if (T::cnt(sg) > 0) av[sg] = base[G::BSTR * (T::row(sg) >= 0 ? T::row(sg) : 0)] * wr;
     }
@@ -745,11 +812,11 @@ __device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lan
   }
 }
 
-template <int FAM, int LNK, int WV>
+template <int P16, int FAM, int LNK, int WV>
 __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int lane) {
-  using G = Geo<16>;
-  using R = GeoR;
-  using T = TilesR<WV>;
+  using G = Geo<P16>;
+  using R = GeoR<P16>;
+  using T = TilesR<P16, WV>;
   constexpr bool row_wave = T::ROW;
   constexpr int si = row_wave ? WV - 8 : 0;  // DMA issuer index (row waves)
   constexpr int wv = WV;                     // (SGLM_STAMP)
@@ -772,8 +839,8 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   for (int k = 0; k < 4; ++k) voff[k] = (uint32_t)(((int64_t)lcq * a.ld + ((2 * li) ^ ((8 * k + 2 * lcq) & 31))) * 8);
   const uint32_t vvoff = (uint32_t)(lane < 16 ? 16 * lane : 16 * 16);
   if (row_wave && b0 < b1) {
-    stage_block_r(lds, 0, a, b0, si, voff, vvoff);
-    if (b0 + 1 < b1) stage_block_r(lds, 1, a, b0 + 1, si, voff, vvoff);
+    stage_block_r<P16>(lds, 0, a, b0, si, voff, vvoff);
+    if (b0 + 1 < b1) stage_block_r<P16>(lds, 1, a, b0 + 1, si, voff, vvoff);
   }
   if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(SGLM_K1R_PRIO_ALT ? 2 : 1);
 #if SGLM_K1R_ASYNC
@@ -797,11 +864,11 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   };
   if constexpr (row_wave) {
     if (b0 < b1) {
-      if (b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
+      if (b0 + 1 < b1) wait_vmcnt<R::QPW + 1>();
       else wait_vmcnt<0>();
       bump(flag);
       spin(flag, 4u);
-      if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
+      if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
       bump(ready);
     }
 #pragma unroll 1
@@ -815,20 +882,20 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
         bump(flag);
         spin(flag, (unsigned)(4 * (blk + 2 - b0)));
         SGLM_STAMP(3);
-        if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+        if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
         bump(ready);
       }
       SGLM_STAMP(4);
       // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them
       // (each row wave bumps flag after its row stage of blk); the last block has no such round
       if (blk + 1 >= b1) spin(ready, (unsigned)(4 * (blk - b0 + 1)));
-      if (do_gram) xz_rows_r(lds, cur, si, lane, xz);
+      if (do_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
       SGLM_STAMP(5);
       bump(done);  // this row wave's reads of block blk (X'Wz) are complete
       if (blk + 2 < b1) {
         spin(done, (unsigned)(12 * (blk - b0 + 1)));
         SGLM_STAMP(6);
-        if (!(SGLM_DBG(a) & 4)) stage_block_r(lds, cur, a, blk + 2, si, voff, vvoff);
+        if (!(SGLM_DBG(a) & 4)) stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
       }
       SGLM_STAMP(7);
     }
@@ -839,7 +906,7 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
       SGLM_STAMP(0);
       spin(ready, (unsigned)(4 * (blk - b0 + 1)));
       SGLM_STAMP(1);
-      if (do_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+      if (do_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
       SGLM_STAMP(2);
       SGLM_STAMP(3);
       SGLM_STAMP(4);
@@ -860,14 +927,14 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
     const bool has_gram = has_gram_ct && do_gram;
     SGLM_STAMP(0);
     if constexpr (!row_wave)
-      if (has_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+      if (has_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
     if constexpr (row_wave)
-      if (has_gram) xz_rows_r(lds, cur, si, lane, xz);
+      if (has_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
     SGLM_STAMP(1);
     if constexpr (row_wave) {
       if (blk + 1 < b1) {
         // own part of block blk+1 landed (block b0+1 may still be in flight behind b0)
-        if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
+        if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<R::QPW + 1>();
         else wait_vmcnt<0>();
         SGLM_STAMP(2);
         if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -875,16 +942,16 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
         while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
           __builtin_amdgcn_s_sleep(1);
         SGLM_STAMP(3);
-        if (!(SGLM_DBG(a) & 1)) row_stage_r<FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+        if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
       }
     }
     SGLM_STAMP(4);
     if constexpr (row_wave && T::NT > 0)  // the row waves' tiles, after the row stage
-      if (has_gram) gram_steps_r<WV>(lds, cur, lane, acc);
+      if (has_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
     SGLM_STAMP(5);
     lds_barrier();
     SGLM_STAMP(6);
-    if (row_wave && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block_r(lds, cur, a, blk + 2, si, voff, vvoff);
+    if (row_wave && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
     SGLM_STAMP(7);
   };
   if (b0 < b1) iteration(b0 - 1, std::false_type{});
@@ -905,11 +972,11 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   }
   if constexpr (row_wave) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < XzBlocks<P16, si>::N; ++b) {
       double v = xz[b];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      if (lane < 16) out[G::T * 256 + 16 * (4 * si + b) + lane] = v;
+      if (lane < 16) out[G::T * 256 + 16 * (XzBlocks<P16, si>::LO + b) + lane] = v;
     }
   }
 #pragma unroll
@@ -937,39 +1004,40 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   }
 }
 
-template <int FAM, int LNK>
-__global__ void __launch_bounds__(64 * GeoR::NW, 3) irls_pass_r_kernel(PassArgs a) {
-  using G = Geo<16>;
-  __shared__ double lds[GeoR::LDS_DOUBLES];
+template <int P16, int FAM, int LNK>
+__global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(PassArgs a) {
+  using G = Geo<P16>;
+  using R = GeoR<P16>;
+  __shared__ double lds[R::LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int c = threadIdx.x; c < G::NCE; c += 64 * GeoR::NW) {
+  for (int c = threadIdx.x; c < G::NCE; c += 64 * R::NW) {
     const double b = (a.beta && c < a.p) ? a.beta[c] : 0.0;
     lds[G::OFF_BETA + c] = b;
     // betag[g][t * 4 + u] = beta[4 g + u + 32 t] (row_stage_r)
-    lds[GeoR::OFF_BETAG + ((c & 31) >> 2) * GeoR::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
+    lds[R::OFF_BETAG + ((c & 31) >> 2) * R::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
   }
-  if (threadIdx.x < 3) ((unsigned*)(lds + GeoR::OFF_FLAG))[threadIdx.x] = 0u;
+  if (threadIdx.x < 3) ((unsigned*)(lds + R::OFF_FLAG))[threadIdx.x] = 0u;
   if constexpr (FAM == FAM_BINOMIAL)
     if (threadIdx.x == 0 && init_fast_row(FAM, a.mode, a.m != nullptr)) {
       const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
-      for (int k = 0; k < 6; ++k) lds[GeoR::OFF_INIT + k] = ic.v[k];
+      for (int k = 0; k < 6; ++k) lds[R::OFF_INIT + k] = ic.v[k];
     }
   SGLM_HWID(wv);
   __syncthreads();
   switch (wv) {
-    case 0: pass_body_r<FAM, LNK, 0>(lds, a, lane); break;
-    case 1: pass_body_r<FAM, LNK, 1>(lds, a, lane); break;
-    case 2: pass_body_r<FAM, LNK, 2>(lds, a, lane); break;
-    case 3: pass_body_r<FAM, LNK, 3>(lds, a, lane); break;
-    case 4: pass_body_r<FAM, LNK, 4>(lds, a, lane); break;
-    case 5: pass_body_r<FAM, LNK, 5>(lds, a, lane); break;
-    case 6: pass_body_r<FAM, LNK, 6>(lds, a, lane); break;
-    case 7: pass_body_r<FAM, LNK, 7>(lds, a, lane); break;
-    case 8: pass_body_r<FAM, LNK, 8>(lds, a, lane); break;
-    case 9: pass_body_r<FAM, LNK, 9>(lds, a, lane); break;
-    case 10: pass_body_r<FAM, LNK, 10>(lds, a, lane); break;
-    default: pass_body_r<FAM, LNK, 11>(lds, a, lane); break;
+    case 0: pass_body_r<P16, FAM, LNK, 0>(lds, a, lane); break;
+    case 1: pass_body_r<P16, FAM, LNK, 1>(lds, a, lane); break;
+    case 2: pass_body_r<P16, FAM, LNK, 2>(lds, a, lane); break;
+    case 3: pass_body_r<P16, FAM, LNK, 3>(lds, a, lane); break;
+    case 4: pass_body_r<P16, FAM, LNK, 4>(lds, a, lane); break;
+    case 5: pass_body_r<P16, FAM, LNK, 5>(lds, a, lane); break;
+    case 6: pass_body_r<P16, FAM, LNK, 6>(lds, a, lane); break;
+    case 7: pass_body_r<P16, FAM, LNK, 7>(lds, a, lane); break;
+    case 8: pass_body_r<P16, FAM, LNK, 8>(lds, a, lane); break;
+    case 9: pass_body_r<P16, FAM, LNK, 9>(lds, a, lane); break;
+    case 10: pass_body_r<P16, FAM, LNK, 10>(lds, a, lane); break;
+    default: pass_body_r<P16, FAM, LNK, 11>(lds, a, lane); break;
   }
 }
 
@@ -1197,9 +1265,19 @@ int pass_wg_per_cu(int P16) {
 
 // One kernel per (column-block count, family/link): the row stage is compiled for a
 // single family so its registers fit beside the resident Gram accumulators.
-template <int FAM, int LNK>
+template <int P16, int FAM, int LNK>
 static void launch_pass_r(const PassArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((irls_pass_r_kernel<FAM, LNK>), dim3(grid), dim3(64 * GeoR::NW), 0, st, a);
+  hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM, LNK>), dim3(grid), dim3(64 * GeoR<P16>::NW), 0, st, a);
+}
+
+// K1r runs column-block counts P16 >= the threshold PassArgs::fused_split carries (1: the default
+// SGLM_K1R_MIN_P16, 0: never) -- one 12-wave workgroup per CU; K1 the rest.
+#ifndef SGLM_K1R_MIN_P16
+#define SGLM_K1R_MIN_P16 16
+#endif
+bool pass_uses_split(int P16, int fused_split, int64_t ld) {
+  const int thr = fused_split == 1 ? SGLM_K1R_MIN_P16 : fused_split;
+  return fused_split != 0 && P16 >= 6 && P16 >= thr && ld * 24 + 4096 < ((int64_t)1 << 32);
 }
 
 template <int P16>
@@ -1210,13 +1288,14 @@ static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st) {
   // the split-role kernel (K1r) for the widest fused variant; its DMA addresses the 4 columns
   // of a quad by 32-bit lane offsets (3 ld + 32 rows, in bytes), which bounds the shard at ~178M
   // rows (a p = 256 shard that size would not fit in HBM anyway)
-  if (P16 == 16 && a.fused_split && a.ld * 24 + 4096 < ((int64_t)1 << 32)) {
-    if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT) launch_pass_r<FAM_BINOMIAL, LNK_LOGIT>(a, grid, st);
-    else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT) launch_pass_r<FAM_BINOMIAL, LNK_PROBIT>(a, grid, st);
-    else if (mode_fam == FAM_BINOMIAL) launch_pass_r<FAM_BINOMIAL, LNK_CLOGLOG>(a, grid, st);
-    else if (mode_fam == FAM_GAUSSIAN) launch_pass_r<FAM_GAUSSIAN, LNK_IDENTITY>(a, grid, st);
-    else if (mode_fam == FAM_POISSON) launch_pass_r<FAM_POISSON, LNK_LOG>(a, grid, st);
-    else if (mode_fam == FAM_GAMMA) launch_pass_r<FAM_GAMMA, LNK_INVERSE>(a, grid, st);
+  if constexpr (P16 >= 6)
+  if (pass_uses_split(P16, a.fused_split, a.ld)) {
+    if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT) launch_pass_r<P16, FAM_BINOMIAL, LNK_LOGIT>(a, grid, st);
+    else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT) launch_pass_r<P16, FAM_BINOMIAL, LNK_PROBIT>(a, grid, st);
+    else if (mode_fam == FAM_BINOMIAL) launch_pass_r<P16, FAM_BINOMIAL, LNK_CLOGLOG>(a, grid, st);
+    else if (mode_fam == FAM_GAUSSIAN) launch_pass_r<P16, FAM_GAUSSIAN, LNK_IDENTITY>(a, grid, st);
+    else if (mode_fam == FAM_POISSON) launch_pass_r<P16, FAM_POISSON, LNK_LOG>(a, grid, st);
+    else if (mode_fam == FAM_GAMMA) launch_pass_r<P16, FAM_GAMMA, LNK_INVERSE>(a, grid, st);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

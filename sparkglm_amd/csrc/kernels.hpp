@@ -12,6 +12,7 @@ int pass_variant(int p);        // column-block count P16 of the kernel instanti
 int pass_waves(int P16);        // waves per workgroup of that variant
 int pass_stride(int P16);       // doubles per workgroup partial
 int pass_wg_per_cu(int P16);    // workgroups per CU the variant is built for
+bool pass_uses_split(int P16, int fused_split, int64_t ld);  // K1r (one 12-wave workgroup per CU) for this pass
 hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st);
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st);

@@ -1273,7 +1273,7 @@ static void launch_pass_r(const PassArgs& a, int grid, hipStream_t st) {
 // K1r runs column-block counts P16 >= the threshold PassArgs::fused_split carries (1: the default
 // SGLM_K1R_MIN_P16, 0: never) -- one 12-wave workgroup per CU; K1 the rest.
 #ifndef SGLM_K1R_MIN_P16
-#define SGLM_K1R_MIN_P16 16
+#define SGLM_K1R_MIN_P16 10
 #endif
 bool pass_uses_split(int P16, int fused_split, int64_t ld) {
   const int thr = fused_split == 1 ? SGLM_K1R_MIN_P16 : fused_split;

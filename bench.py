@@ -300,7 +300,8 @@ def main() -> int:
             pass_ms = kern_ms
         else:
             p16 = (p + 15) // 16 + ((p + 15) // 16) % 2
-            if p16 == 16 and os.environ.get("SGLM_FUSED_SPLIT", "1") != "0":  # K1r (engine.cpp fused_split)
+            fs = int(os.environ.get("SGLM_FUSED_SPLIT", "1") or 0)  # engine.cpp fused_split, kernels.hip pass_uses_split
+            if fs != 0 and p16 >= max(6, 10 if fs == 1 else fs):  # K1r
                 kern = f"irls_pass_r_kernel<{fam},{lnk}> (K1r, split-role fused pass)"
             else:
                 kern = f"irls_pass_kernel<{p16},{fam},{lnk}>"

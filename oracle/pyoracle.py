@@ -58,6 +58,8 @@ def lib():
         _lib.orc_fit_glm_synth.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64,
                                            C.POINTER(_Opts), C.POINTER(_Pre)]
         _lib.orc_synth_rows.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, dp, dp, dp, dp]
+        _lib.orc_pass_synth.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_int, C.c_int,
+                                        C.c_int, dp, C.c_double, C.c_int, dp, dp, dp]
         for f in ("orc_norm_cdf", "orc_norm_icdf", "orc_erfinv"):
             getattr(_lib, f).argtypes = [C.c_double]
             getattr(_lib, f).restype = C.c_double
@@ -128,6 +130,18 @@ def fit_glm_synth(kind, row0, n, p, seed, family="binomial", link="logit", *, to
         raise RuntimeError(f"oracle orc_fit_glm_synth failed rc={rc}")
     return OraclePreGLM(coefs, se, pre.deviance, pre.null_deviance, pre.pearson, pre.loglik,
                         pre.iter, pre.nrow, pre.npart, trace[: pre.iter + 1].copy())
+
+
+def pass_synth(kind, row0, n, p, seed, family, link, beta=None, mu0=0.0, mode=0, nthreads=8):
+    """One pass of the streaming fit (orc_pass_synth) at beta: (X'WX p x p, X'Wz, scalars[8])."""
+    G, xtwz, s = np.zeros((p, p), order="F"), np.zeros(p), np.zeros(NS)
+    b = None if beta is None else np.ascontiguousarray(beta, dtype=np.float64)
+    rc = lib().orc_pass_synth(int(kind), int(row0), int(n), int(p), C.c_uint64(seed & (2**64 - 1)),
+                              FAMILIES[family], LINKS[link], int(mode), _ptr(b), float(mu0), int(nthreads),
+                              G.ctypes.data_as(C.POINTER(C.c_double)), _ptr(xtwz), _ptr(s))
+    if rc != 0:
+        raise RuntimeError(f"oracle orc_pass_synth failed rc={rc}")
+    return G, xtwz, s
 
 
 def synth_rows(kind, row0, n, p, seed):

@@ -858,6 +858,28 @@ static void seg_total(const seg_acc *seg, int64_t p, int with_gram, double *G, d
   if (with_gram) symmetrize_lower(G, p);
 }
 
+/* One streaming pass of orc_fit_glm_synth at beta (its IRLS passes, GLM.scala:453-458 over the
+ * generated rows): X'WX (p*p col-major, symmetric), X'Wz and the 8 scalars, summed exactly as the
+ * fit sums them.  For comparing the engine's Gram with the oracle's at the same beta. */
+int orc_pass_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, int family, int link, int mode,
+                   const double *beta, double mu0, int nthreads, double *G, double *xtwz, double *s) {
+  if (kind < 0 || kind > 3 || n <= 0 || p <= 0 || !G || !xtwz || !s) return ORC_EINVAL;
+  if (mode == ORC_MODE_IRLS && !beta) return ORC_EINVAL;
+  orc_gen g;
+  gen_init(&g, kind, p, seed);
+  seg_acc *seg = (seg_acc *)calloc(ORC_NSEG, sizeof(seg_acc));
+  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) {
+    seg[sgi].G = (double *)calloc((size_t)(p * p), sizeof(double));
+    seg[sgi].xtwz = (double *)calloc((size_t)p, sizeof(double));
+  }
+  stream_pass(&g, row0, n, family, link, mode, beta, mu0, nthreads, seg, 0);
+  seg_total(seg, p, 1, G, xtwz, s, 0);
+  for (int sgi = 0; sgi < ORC_NSEG; ++sgi) { free(seg[sgi].G); free(seg[sgi].xtwz); }
+  free(seg);
+  free(g.bs);
+  return ORC_OK;
+}
+
 int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, const orc_opts *o,
                       orc_preglm *out) {
   if (kind < 0 || kind > 3 || n <= 0 || p <= 0) return ORC_EINVAL;

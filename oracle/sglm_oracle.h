@@ -84,6 +84,10 @@ int orc_shard_partials(const double *X, int64_t n, int64_t p, int64_t ldx,
  * fitMultipleBinomial first step; m = 1.  Same outputs as orc_fit_glm. */
 int orc_fit_glm_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, const orc_opts *opts,
                       orc_preglm *out);
+/* One pass of that streaming fit at beta (mode ORC_MODE_IRLS) or at mu0 (init modes): G [p*p]
+ * col-major symmetric X'WX, xtwz [p], s [8] scalars, summed as orc_fit_glm_synth sums them. */
+int orc_pass_synth(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, int family, int link, int mode,
+                   const double *beta, double mu0, int nthreads, double *G, double *xtwz, double *s);
 /* The generator itself (X column-major with ld = n; offset / prior only for kind 2, may be NULL). */
 int orc_synth_rows(int kind, int64_t row0, int64_t n, int64_t p, uint64_t seed, double *X, double *y,
                    double *offset, double *prior);

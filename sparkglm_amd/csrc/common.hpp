@@ -36,14 +36,6 @@ inline int64_t tri_count(int64_t p) { return p * (p + 1) / 2; }
 inline int64_t packed_len(int64_t p) { return tri_count(p) + p + NS; }
 
 // Arguments of one fused pass launch.
-// Profiling ablations (SGLM_DEBUG_ABLATE, tools/ablate.py) exist only in the ablation build
-// (make ablate: -DSGLM_ABLATE=1, sparkglm_amd/lib_ablate/); the product kernels compile them
-// out so their main loops carry no debug branches.
-#ifndef SGLM_ABLATE
-#define SGLM_ABLATE 0
-#endif
-#define SGLM_DBG(a) (SGLM_ABLATE ? (a).dbg : 0)
-
 struct PassArgs {
   const double* X;      // col-major, leading dimension ld, 4*nq columns (zero past p)
   int64_t ld;
@@ -66,8 +58,6 @@ struct PassArgs {
                         // pass's scalars instead of the eta store + stats_kernel
   int no_gram;          // deviance-only pass (glm_drive's speculative last pass): row stage, no Gram
   int fused_split;      // split-role kernel K1r (irls_pass_r_kernel) from P16 >= threshold: 1 default, 0 never, N: P16 >= N
-  int dbg;              // ablation bits (profiling): 1 row stage, 2 MFMA, 4 DMA, 8 eta dot, 16 family math,
-                        // 32 no eta store
 };
 
 // ---- wide-design path (p > 16*MAX_P16): row kernel + panel-pair Gram kernel ----
@@ -127,7 +117,6 @@ struct WideGramArgs {
   const int* wg_begin;  // [grid + 1]: pieces of workgroup g are [wg_begin[g], wg_begin[g+1])
   double* partials;     // [slots][stride]
   int64_t stride;
-  int dbg;              // profiling ablations: 4 DMA, 32 barriers
   ProcX proc;
   int64_t nb_lim;       // blocks of this launch's rows: pieces are clipped to [b0, min(b1, nb_lim))
 };

@@ -172,15 +172,13 @@ struct sglm_engine : public Backend {
   double dev_const = 0.0;      // the fit's initial-pass S_AUX1 (Poisson): sum pw y log y, the deviance's constant part
   bool lp_devsplit = false;    // the last pass summed the Poisson deviance without that constant (narrow)
   int consts_family = -1;      // family whose initial pass produced stats_const / dev_const on this data (-1: none)
-  bool stats_every_pass = false;  // SGLM_STATS_EVERY_PASS=1: Poisson / Gamma statistics in every pass (A/B)
-  bool force_eta_store = false;  // SGLM_ETA_STORE=1: always the eta store + stats_kernel (tests)
   // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
   // scalar reduction but no Gram -- bitwise the scalars of the full pass.  SGLM_SPECULATE=0 off.
   bool dev_only = false, allow_spec = true;
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
-  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; SGLM_NARROW=0 disables
-  bool narrow = false, allow_narrow = true;
+  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines
+  bool narrow = false;
   // procedural shard (sglm_synth_procedural): X regenerated in the wide kernels, not stored
   ProcX procx{};
   // procedural shards in chunks (setup_proc_chunks): each pass generates C rows of X at a time
@@ -206,7 +204,6 @@ struct sglm_engine : public Backend {
   int nov = 0;
   int64_t ov_rows = 0;             // rows per chunk (multiple of 32; the last chunk may be shorter)
   int rgrid_ov = 0;                // row-kernel grid of chunks >= 1 (one workgroup per CU)
-  bool ov_serial = false;          // SGLM_WIDE_OV_SERIAL=1: the chunks' row kernels on st (A/B only)
   hipStream_t st2 = nullptr;
   std::vector<hipEvent_t> evov;    // [4 * nov + 1]: row span, Gram span per chunk; st -> st2 fork
   double *dw = nullptr, *dwz = nullptr, *dgp = nullptr, *drp = nullptr;
@@ -227,7 +224,6 @@ struct sglm_engine : public Backend {
   int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
-  int dbg = 0;  // profiling ablations (SGLM_DEBUG_ABLATE), never set in production
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
   static constexpr int64_t STAGE_DOUBLES = (int64_t)8 << 20;  // 64 MiB each
   double* hstage[2] = {nullptr, nullptr};
@@ -445,7 +441,7 @@ struct sglm_engine : public Backend {
   // into ggrid equal segments; a segment's runs inside one super-tile are its pieces.
   // Pieces are numbered in line order, so the partial slots of a super-tile are consecutive.
   //
-  // Banded schedule (wide_band): the k = ggrid / S workgroups of each of the S super-tiles take
+  // Banded schedule: the k = ggrid / S workgroups of each of the S super-tiles take
   // its blocks round-robin (block stride k), so all S k workgroups sweep the rows together and a
   // block read by one super-tile's workgroup is read by the others' while it is still in the
   // Infinity Cache / L2 (the workgroups that read the same blocks are numbered onto the same XCD,
@@ -453,8 +449,8 @@ struct sglm_engine : public Backend {
   // E / ggrid of every super-tile's blocks cut into E equal contiguous segments, so no workgroup
   // idles and each carries the same work.  Slots of a super-tile: its k strided pieces, then its
   // tail pieces in row order (the fixed reduction order).
-  int wide_band = 1;  // SGLM_WIDE_BAND: 0 contiguous cost-balanced pieces, 1 banded
-  bool banded_kind(int S, int64_t nb, int G) const { return wide_band != 0 && S > 0 && G / S >= 2 && nb >= 2; }
+  // (shards too short to give every super-tile two workgroups keep the contiguous pieces)
+  bool banded_kind(int S, int64_t nb, int G) const { return S > 0 && G / S >= 2 && nb >= 2; }
   int build_wide_schedule() {
     const int64_t nb = (nch > 0 ? ch_rows : nov > 0 ? ov_rows : n_pad) / WIDE_RB;
     std::vector<int> str((size_t)nst * 2, 0);
@@ -654,7 +650,7 @@ struct sglm_engine : public Backend {
       int rc = ensure_wide_workspace();
       if (rc) return rc;
     }
-    narrow = !wide && allow_narrow && p <= 64;
+    narrow = !wide && p <= 64;
     if (narrow) {
       P16 = narrow_variant((int)p);
       stride = narrow_stride(P16);
@@ -1056,14 +1052,12 @@ struct sglm_engine : public Backend {
     // +14 % per pass (125M x 64 Poisson: 17.4 against 15.3 ms, tools/ab_stats.py; the family
     // arithmetic runs on 16 of 64 lanes there), while the deviance-only pass has no Gram to slow.
     a.stats_in_pass = (narrow && mode == MODE_IRLS && stats_in_pass_family(family, link) &&
-                       !(family == FAM_BINOMIAL && dm) && !force_eta_store &&
-                       (family == FAM_BINOMIAL || dev_only || stats_every_pass)) ? 1 : 0;
+                       !(family == FAM_BINOMIAL && dm) && (family == FAM_BINOMIAL || dev_only)) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
     lp_devsplit = narrow && mode == MODE_IRLS && family == FAM_POISSON;  // narrow.hip: pass_row dev_nolog
-    a.eta_out = (mode == MODE_IRLS && !(dbg & 32) && !a.stats_in_pass) ? deta : nullptr;
+    a.eta_out = (mode == MODE_IRLS && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.fused_split = fused_split;
-    a.dbg = dbg;
     HIPCHK(hipEventRecord(ev0, st));
     if (wide) {
       WideRowArgs r{};
@@ -1097,7 +1091,6 @@ struct sglm_engine : public Backend {
       g.wz = dwz;
       g.partials = dgp;
       g.stride = wstride;
-      g.dbg = dbg;
       g.proc = procx;
       g.nb_lim = INT64_MAX;
       if (nch > 0) {  // procedural shard in chunks: generate C rows into the scratch, resident Gram over it
@@ -1154,9 +1147,9 @@ struct sglm_engine : public Backend {
         for (int c = 0; c < nov; ++c) {
           rows_of(c, r.r_begin, r.r_end);
           r.row_partials = rowpart(c);
-          HIPCHK(hipEventRecord(evov[(size_t)4 * c], ov_serial ? st : st2));
-          HIPCHK(launch_wide_rows(r, c == 0 ? rgrid : rgrid_ov, ov_serial ? st : st2, c > 0));
-          HIPCHK(hipEventRecord(evov[(size_t)4 * c + 1], ov_serial ? st : st2));
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c], st2));
+          HIPCHK(launch_wide_rows(r, c == 0 ? rgrid : rgrid_ov, st2, c > 0));
+          HIPCHK(hipEventRecord(evov[(size_t)4 * c + 1], st2));
         }
         for (int c = 0; c < nov; ++c) {
           int64_t r0 = 0, r1 = 0;
@@ -1646,19 +1639,11 @@ int sglm_create(int device, sglm_engine** out) {
   hipDeviceProp_t prop;
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e, "hipGetDeviceProperties");
   h->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-#if SGLM_ABLATE  // ablation build only (make ablate)
-  if (const char* ab = std::getenv("SGLM_DEBUG_ABLATE")) h->dbg = std::atoi(ab);
-#endif
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
-  if (const char* nw = std::getenv("SGLM_NARROW")) h->allow_narrow = std::atoi(nw) != 0;
-  if (const char* es = std::getenv("SGLM_ETA_STORE")) h->force_eta_store = std::atoi(es) != 0;
-  if (const char* se = std::getenv("SGLM_STATS_EVERY_PASS")) h->stats_every_pass = std::atoi(se) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
-  if (const char* wb = std::getenv("SGLM_WIDE_BAND")) h->wide_band = std::atoi(wb);
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
-  if (const char* os = std::getenv("SGLM_WIDE_OV_SERIAL")) h->ov_serial = std::atoi(os) != 0;
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
   if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::max(0, std::atoi(fs));

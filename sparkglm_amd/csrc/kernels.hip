@@ -23,54 +23,6 @@
 #include "procx.hpp"
 #include "rowmath.hpp"
 
-#ifndef SGLM_K1
-#define SGLM_K1 -1
-#endif
-#ifndef SGLM_KA
-#define SGLM_KA -1
-#endif
-#ifndef SGLM_PRIO
-#define SGLM_PRIO 1
-#endif
-#ifndef SGLM_SPLIT16
-#define SGLM_SPLIT16 19
-#endif
-// K1r's row stage evaluates exp by exp_small (its constants in SGPRs: libm exp's hoisted
-// coefficients pushed the row waves past the 168-VGPR budget of three waves per SIMD)
-#ifndef SGLM_K1R_SMALLEXP
-#define SGLM_K1R_SMALLEXP 1
-#endif
-
-#ifdef SGLM_STAMPS
-// Diagnostic build only (tools/stamps.py): per-phase s_memtime stamps of workgroup 0's waves
-// over 16 steady-state blocks.  [wave 12][block 16][event 8]
-__device__ unsigned long long sglm_stamp_buf[12 * 16 * 8];
-#define SGLM_STAMP(ev)                                                                          \
-  do {                                                                                          \
-    if (blockIdx.x == 0 && blk >= b0 + 100 && blk < b0 + 116 && lane == 0)                      \
-      sglm_stamp_buf[(wv * 16 + (int)(blk - b0 - 100)) * 8 + (ev)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-extern "C" int sglm_debug_stamps(unsigned long long* out, long count) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_stamp_buf), sizeof(unsigned long long) * count);
-}
-// HW_ID (SIMD id in bits 5:4) of every wave of workgroup 0
-__device__ unsigned sglm_hwid_buf[16];
-#define SGLM_HWID(wv)                                                                                  \
-  do {                                                                                                 \
-    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) sglm_hwid_buf[wv] = __builtin_amdgcn_s_getreg(4 | (31 << 11)); \
-  } while (0)
-extern "C" int sglm_debug_hwid(unsigned* out, long count) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_hwid_buf), sizeof(unsigned) * count);
-}
-#else
-#define SGLM_STAMP(ev) \
-  do {                 \
-  } while (0)
-#define SGLM_HWID(wv) \
-  do {                \
-  } while (0)
-#endif
-
 namespace sglm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -123,28 +75,18 @@ struct Geo {
   // stage on top of their MFMAs, so they take the LOW rows 0..NRW-1 (fewest tiles) and the
   // first NRW MFMA-only waves take ROW0.. in exchange (P16 = 16: 13 tiles per row wave, 21
   // per MFMA-only wave 0-3, instead of 17 everywhere).
-  // P16 = 16 uses SPLIT16 (row waves 15 / MFMA-only waves 19 tiles: a 13 / 21 split would
-  // not fit the 256-VGPR budget of two waves per SIMD).
-  static constexpr int SPLIT16 = SGLM_SPLIT16;
+  // P16 = 16: row waves 15 / MFMA-only waves 19 tiles (a 13 / 21 split would not fit the
+  // 256-VGPR budget of two waves per SIMD; 17 / 17 and 16 / 18 measured slower).
   static constexpr int lo_row(int wv) {
-    if (P16 == 16 && SPLIT16 == 19) {
+    if (P16 == 16) {
       constexpr int t[8] = {2, 3, 6, 7, 0, 1, 4, 5};
       return t[wv];
     }
-    if (P16 == 16 && SPLIT16 == 18) {
-      constexpr int t[8] = {1, 3, 5, 7, 0, 2, 4, 6};
-      return t[wv];
-    }
-    if ((P16 == 16 && SPLIT16 == 17) || SPLIT16 == 0) return wv;  // 0: no exchange at any P16
     return wv < NRW ? ROW0 + wv : (wv >= ROW0 && wv < ROW0 + NRW ? wv - ROW0 : wv);
   }
   static constexpr int hi_row(int wv) {
-    if (P16 == 16 && SPLIT16 == 19) {
+    if (P16 == 16) {
       constexpr int t[8] = {15, 14, 11, 10, 13, 12, 9, 8};
-      return t[wv];
-    }
-    if (P16 == 16 && SPLIT16 == 18) {
-      constexpr int t[8] = {15, 13, 11, 9, 14, 12, 10, 8};
       return t[wv];
     }
     return P16 - 1 - wv;
@@ -244,7 +186,7 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
   const int rl = lane % G::RW, g = lane / G::RW;
   const int r = G::RW * rw + rl;
   double eta = 0.0;
-  if (a.mode == MODE_IRLS && !(SGLM_DBG(a) & 8)) {
+  if (a.mode == MODE_IRLS) {
     // four independent partial sums per lane shorten the dependent FMA chain
     double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -272,14 +214,13 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
         eta = eta + off;
         if (a.eta_out) a.eta_out[row] = eta;
       }
-      if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
       // initial pass (binomial, no m): the per-pass constants from LDS (bitwise pass_row_ref's rows)
-      else if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
+      if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
         pass_row_init(lds + G::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
       // (P16 = 16: the row arithmetic of K1r's row_stage_r, so that K1 and K1r are bitwise
       // interchangeable -- tests/test_gpu_fused_split.py)
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux,
-                    P16 == 16 && SGLM_K1R_SMALLEXP);
+                    P16 == 16);
     }
     lds[G::OFF_W + wb * 2 * RB + r] = w;
     lds[G::OFF_W + wb * 2 * RB + RB + r] = wz;
@@ -332,13 +273,13 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
 // Only the end-of-block barrier orders the image and the w buffers across all waves.  The
 // DMA issue (a burst the memory queues throttle to ~5k cycles per block) sits on the issuers,
 // which have slack at the barrier; the row waves carry the critical path (their MFMAs + the
-// row stage) at raised priority.  Measured per-phase with tools/stamps.py (-DSGLM_STAMPS).
+// row stage) at raised priority (per-phase s_memtime stamps, round 2: DESIGN.md 4 K1).
 template <int P16, int FAM, int LNK, int WV>
 __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv, int lane) {
   using G = Geo<P16>;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
-  const bool do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram;
+  const bool do_gram = !a.no_gram;
   // roles are compile-time per wave (WV), so each wave's instantiation carries only its code
   constexpr int rw = WV - G::ROW0;
   constexpr bool row_wave = rw >= 0 && rw < G::NRW;
@@ -347,8 +288,8 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   constexpr int si = G::NA > 0 ? (WV < G::ROW0 ? WV : WV - G::NRW) : 0;
   // MFMA k-steps of block i before the row stage of block i+1 (K1) and before an issuer
   // publishes its landed part of block i+1 (KA); A/B-measured per variant (tools/ab.py)
-  constexpr int K1 = SGLM_K1 >= 0 ? SGLM_K1 : (P16 == 16 ? 7 : 6);
-  constexpr int KA = SGLM_KA >= 0 ? SGLM_KA : (P16 == 16 ? 0 : 2);
+  constexpr int K1 = P16 == 16 ? 7 : 6;
+  constexpr int KA = P16 == 16 ? 0 : 2;
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
   d4 acc[G::ntiles(WV)];
@@ -360,7 +301,7 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     stage_block<P16>(lds, 0, a, b0, si, lane);
     if (b0 + 1 < b1) stage_block<P16>(lds, 1, a, b0 + 1, si, lane);
   }
-  if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(1);
+  if (row_wave) __builtin_amdgcn_s_setprio(1);
   // Iteration blk runs the MFMA phase of block blk and the row stage of block blk+1.  The
   // first iteration (blk = b0-1: row stage of b0 only) is peeled so that the steady-state loop
   // carries no branch around its MFMA phases (HG: has_gram, compile-time).
@@ -369,33 +310,24 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     constexpr bool has_gram_ct = decltype(HG)::value;
     const bool has_gram = has_gram_ct && do_gram;
     const bool has_next = blk + 1 < b1;
-    SGLM_STAMP(0);
     if constexpr (G::NA > 0) {
       if constexpr (!row_wave) {
         // MFMA-only wave: after KA k-steps, publish that its part of block blk+1 has landed
         if (has_gram) gram_steps<P16, WV, KA>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
-        SGLM_STAMP(1);
         if (has_next) {
           wait_vmcnt<0>();
-          SGLM_STAMP(2);
           if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        SGLM_STAMP(3);
-        SGLM_STAMP(4);
         if (has_gram) gram_steps<P16, WV, RB / 4 - KA>(lds, cur & 1, cur & 1, lane, KA, acc, xz_lo, xz_hi);
       } else {
         // row wave: after K1 k-steps, wait until every issuer's part of block blk+1 landed
         if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
-        SGLM_STAMP(1);
-        SGLM_STAMP(2);
         if (has_next) {
           const unsigned target = (unsigned)(G::NA * (blk + 2 - b0));
           while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
             __builtin_amdgcn_s_sleep(1);
-          SGLM_STAMP(3);
-          if (!(SGLM_DBG(a) & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+          row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
         }
-        SGLM_STAMP(4);
         if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
       }
     } else {
@@ -404,15 +336,12 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
       if (has_next) {
         if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
         else wait_vmcnt<0>();
-        if (!(SGLM_DBG(a) & 1)) row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
+        row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
       }
       if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
     }
-    SGLM_STAMP(5);
     lds_barrier();
-    SGLM_STAMP(6);
-    if (issuer && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
-    SGLM_STAMP(7);
+    if (issuer && blk >= b0 && blk + 2 < b1) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
   };
   if (b0 < b1) iteration(b0 - 1, std::false_type{});
 #pragma unroll 1
@@ -473,7 +402,6 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
       const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
       for (int k = 0; k < 6; ++k) lds[G::OFF_INIT + k] = ic.v[k];
     }
-  SGLM_HWID(wv);
   if constexpr (G::NCE > G::NC) {  // LDS columns no DMA writes: keep them finite (zero)
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * G::NW) {
       const int c = G::NC + e / RB, r = e % RB;
@@ -495,12 +423,12 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
 }
 
 // ---------------------------------------------------------------------------------
-// K1r: the split-role fused pass for P16 = 16 (225 <= p <= 256, BASELINE configs[1]).
-// 12 waves, three per SIMD: two "Gram waves" and one "row wave" on every SIMD.
-//   Gram waves 0..7: 16 lower-triangle tiles each, nothing but the block's MFMAs (A scaled by
-//                    w, X'Wz on the VALU) -- the SIMD always has an MFMA stream ready;
+// K1r: the split-role fused pass (P16 >= 10 by default; P16 = 16: 225 <= p <= 256, BASELINE
+// configs[1]).  12 waves, three per SIMD: two "Gram waves" and one "row wave" on every SIMD.
+//   Gram waves 0..7: 17 lower-triangle tiles each at P16 = 16, nothing but the block's MFMAs
+//                    (A scaled by w) -- the SIMD always has an MFMA stream ready;
 //   row waves 8..11: the LDS-DMA of the blocks, the row stage of the next block (eta, mu, w,
-//                    w*z, deviance) and the two tiles (7, 2k), (7, 2k+1) of block row 7.
+//                    w*z, deviance) and X'Wz.
 // In K1 (pass_body) the row stage ran on a wave that also carried 15 tiles: its dependent fp64
 // chain waited one partner MFMA (64 cycles) per instruction, and the partner wave ran out of
 // MFMAs before the row stage ended (phase stamps: ~3.2K idle cycles per 23.2K-cycle block).
@@ -508,24 +436,11 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
 // block; the row waves run it at raised priority, so its VALU issues into the MFMA gaps.
 // Every tile and X'Wz row accumulates the same values in the same order as K1 (same k-steps,
 // same blocks, same lanes), so the partials are bitwise K1's.
-// Tile ownership: Gram wave 0 = block row 15 (16 tiles); Gram wave g = 1..7 = block rows
-// g-1 and 15-g (16 tiles); row wave k = tiles (7, 2k), (7, 2k+1).
+// Tile ownership (P16 = 16): Gram wave 0 = block row 15; Gram wave g = 1..7 = block rows g-1
+// and 15-g; every Gram wave also one tile (7, g) of block row 7 (17 tiles each).  (Measured and
+// not kept: the row waves owning block row 7's tiles after their row stage; a block barrier
+// instead of the LDS counters; no alternating issue priority -- DESIGN.md 4 K1r.)
 // ---------------------------------------------------------------------------------
-#ifndef SGLM_K1R_ASYNC
-#define SGLM_K1R_ASYNC 1
-#endif
-#ifndef SGLM_K1R_PRIO_ALT
-#define SGLM_K1R_PRIO_ALT 1
-#endif
-#ifndef SGLM_K1R_SCHED
-#define SGLM_K1R_SCHED 6
-#endif
-
-// SGLM_K1R_ROWT: 1 = the row waves own block row 7's tiles (two each, after their row stage);
-// 0 = every Gram wave owns one of them (17 tiles per Gram wave, row waves without MFMAs).
-#ifndef SGLM_K1R_ROWT
-#define SGLM_K1R_ROWT 0
-#endif
 
 // A wave's tiles are up to NSEG "segments", each a run of tiles (row, j0 .. j0+cnt-1) of one
 // block row (one A operand per segment, B = column block j).
@@ -557,10 +472,10 @@ struct TilesR {
   static constexpr int thi() { return S::T * (WV + 1) / 8; }
   static constexpr int row(int s) {
     if constexpr (P16 == 16) {
-      if (ROW) return (s == 0 && SGLM_K1R_ROWT) ? 7 : -1;
+      if (ROW) return -1;
       if (s == 0) return WV >= 1 ? WV - 1 : -1;   // LO row
       if (s == 1) return WV == 0 ? 15 : 15 - WV;  // HI row
-      if (s == 2) return SGLM_K1R_ROWT ? -1 : 7;  // one tile of block row 7
+      if (s == 2) return 7;  // one tile of block row 7
       return -1;
     } else {
       if (ROW || thi() <= tlo()) return -1;
@@ -569,13 +484,12 @@ struct TilesR {
     }
   }
   static constexpr int j0(int s) {
-    if constexpr (P16 == 16) return ROW ? 2 * (WV - 8) : (s == 2 ? WV : 0);
+    if constexpr (P16 == 16) return s == 2 ? WV : 0;
     else return s == 0 && !ROW && thi() > tlo() ? tlo() - S::seq_start(S::seq_of(tlo())) : 0;
   }
   static constexpr int cnt(int s) {
     if (row(s) < 0) return 0;
     if constexpr (P16 == 16) {
-      if (ROW) return 2;
       return s == 2 ? 1 : row(s) + 1;
     } else {
       const int i = S::seq_of(tlo()) + s;
@@ -617,7 +531,7 @@ struct GeoR {
   static constexpr bool tiles_ok() {
     return TilesR<P16, 0>::NT + TilesR<P16, 1>::NT + TilesR<P16, 2>::NT + TilesR<P16, 3>::NT + TilesR<P16, 4>::NT +
                TilesR<P16, 5>::NT + TilesR<P16, 6>::NT + TilesR<P16, 7>::NT + (P16 == 16 ? 0 : 0) ==
-           (P16 == 16 && SGLM_K1R_ROWT ? G::T - 8 : G::T);
+           G::T;
   }
   static_assert(tiles_ok(), "the Gram waves' segments cover the tile triangle");
 };
@@ -714,7 +628,7 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
   const double off = a.off ? vv[2 * RB + r] : 0.0;
   const double pw = a.prior ? vv[3 * RB + r] : 1.0;
   double eta = 0.0;
-  if (a.mode == MODE_IRLS && !(SGLM_DBG(a) & 8)) {
+  if (a.mode == MODE_IRLS) {
     double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -750,10 +664,9 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
         eta = eta + off;
         if (a.eta_out) a.eta_out[row] = eta;
       }
-      if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
-      else if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
+      if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
         pass_row_init(lds + GeoR<P16>::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
-      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, SGLM_K1R_SMALLEXP);
+      else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true);
     }
     lds[G::OFF_W + buf * 2 * RB + r] = w;
     lds[G::OFF_W + buf * 2 * RB + RB + r] = wz;
@@ -784,30 +697,24 @@ __device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lan
       const double b = base[G::BSTR * (T::j0(sg) + k - T::off(sg))];
       acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sg], b, acc[k], 0, 0, 0);
     }
-#if SGLM_K1R_SCHED
-    // Keep SGLM_K1R_SCHED B-operand reads in flight ahead of the MFMAs (under the 168-VGPR
-    // budget of three waves per SIMD the default schedule waits for every read in turn):
-    // the A-side reads and the first reads, then one MFMA per further read.
-    __builtin_amdgcn_sched_group_barrier(0x100, 4 + SGLM_K1R_SCHED, 0);
+    // Keep 6 B-operand reads in flight ahead of the MFMAs (under the 168-VGPR budget of three
+    // waves per SIMD the default schedule waits for every read in turn): the A-side reads and the
+    // first reads, then one MFMA per further read.
+    __builtin_amdgcn_sched_group_barrier(0x100, 4 + 6, 0);
 #pragma unroll
     for (int k = 0; k < T::NT; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-#endif
   };
 #pragma unroll 1
   for (int j = 0; j < RB / 4; j += 2) {
-#if SGLM_K1R_PRIO_ALT
     // the two Gram waves of a SIMD take turns at the higher issue priority, one k-step each, so
     // neither runs ahead and leaves the other alone at the end of the block (oldest-first
     // arbitration: waves 0-3 finished their Gram ~7K cycles before waves 4-7)
     if constexpr (!T::ROW) __builtin_amdgcn_s_setprio((WV >> 2) & 1 ? 0 : 1);
-#endif
     kstep(j);
-#if SGLM_K1R_PRIO_ALT
     if constexpr (!T::ROW) __builtin_amdgcn_s_setprio((WV >> 2) & 1 ? 1 : 0);
-#endif
     kstep(j + 1);
   }
 }
@@ -819,11 +726,9 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   using T = TilesR<P16, WV>;
   constexpr bool row_wave = T::ROW;
   constexpr int si = row_wave ? WV - 8 : 0;  // DMA issuer index (row waves)
-  constexpr int wv = WV;                     // (SGLM_STAMP)
-  (void)wv;
   const int wg = blockIdx.x, nwg = gridDim.x;
   const int64_t b0 = (a.nblocks * wg) / nwg, b1 = (a.nblocks * (wg + 1)) / nwg;
-  const bool do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram;
+  const bool do_gram = !a.no_gram;
   unsigned* flag = (unsigned*)(lds + R::OFF_FLAG);
 
   d4 acc[T::NT > 0 ? T::NT : 1];
@@ -842,8 +747,7 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
     stage_block_r<P16>(lds, 0, a, b0, si, voff, vvoff);
     if (b0 + 1 < b1) stage_block_r<P16>(lds, 1, a, b0 + 1, si, voff, vvoff);
   }
-  if (row_wave && SGLM_PRIO) __builtin_amdgcn_s_setprio(SGLM_K1R_PRIO_ALT ? 2 : 1);
-#if SGLM_K1R_ASYNC
+  if (row_wave) __builtin_amdgcn_s_setprio(2);
   // No block barrier: three LDS counters order the ring of two buffers.
   //   flag : +1 per row wave when its LDS-DMA part of a block has landed (4 per block)
   //   ready: +1 per row wave when its rows of a block's row stage are in the w buffer (4 per block)
@@ -868,96 +772,38 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
       else wait_vmcnt<0>();
       bump(flag);
       spin(flag, 4u);
-      if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
+      row_stage_r<P16, FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
       bump(ready);
     }
 #pragma unroll 1
     for (int64_t blk = b0; blk < b1; ++blk) {
       const int cur = (int)((blk - b0) & 1);
-      SGLM_STAMP(0);
-      SGLM_STAMP(1);
       if (blk + 1 < b1) {
         wait_vmcnt<0>();
-        SGLM_STAMP(2);
         bump(flag);
         spin(flag, (unsigned)(4 * (blk + 2 - b0)));
-        SGLM_STAMP(3);
-        if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+        row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
         bump(ready);
       }
-      SGLM_STAMP(4);
       // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them
       // (each row wave bumps flag after its row stage of blk); the last block has no such round
       if (blk + 1 >= b1) spin(ready, (unsigned)(4 * (blk - b0 + 1)));
       if (do_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
-      SGLM_STAMP(5);
       bump(done);  // this row wave's reads of block blk (X'Wz) are complete
       if (blk + 2 < b1) {
         spin(done, (unsigned)(12 * (blk - b0 + 1)));
-        SGLM_STAMP(6);
-        if (!(SGLM_DBG(a) & 4)) stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
+        stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
       }
-      SGLM_STAMP(7);
     }
   } else {
 #pragma unroll 1
     for (int64_t blk = b0; blk < b1; ++blk) {
       const int cur = (int)((blk - b0) & 1);
-      SGLM_STAMP(0);
       spin(ready, (unsigned)(4 * (blk - b0 + 1)));
-      SGLM_STAMP(1);
       if (do_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
-      SGLM_STAMP(2);
-      SGLM_STAMP(3);
-      SGLM_STAMP(4);
-      SGLM_STAMP(5);
       bump(done);
-      SGLM_STAMP(6);
-      SGLM_STAMP(7);
     }
   }
-#else
-  // Iteration blk: the Gram of block blk (buffers cur) on every wave; on the row waves, after
-  // their two tiles, the row stage of block blk+1 (buffers cur ^ 1) once all four row waves'
-  // LDS-DMA of it has landed.  One barrier per block; then the row waves stage block blk+2 into
-  // the buffers block blk has released.
-  auto iteration = [&](int64_t blk, auto HG) {
-    const int cur = (int)((blk - b0) & 1);
-    constexpr bool has_gram_ct = decltype(HG)::value;
-    const bool has_gram = has_gram_ct && do_gram;
-    SGLM_STAMP(0);
-    if constexpr (!row_wave)
-      if (has_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
-    if constexpr (row_wave)
-      if (has_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
-    SGLM_STAMP(1);
-    if constexpr (row_wave) {
-      if (blk + 1 < b1) {
-        // own part of block blk+1 landed (block b0+1 may still be in flight behind b0)
-        if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<R::QPW + 1>();
-        else wait_vmcnt<0>();
-        SGLM_STAMP(2);
-        if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const unsigned target = (unsigned)(4 * (blk + 2 - b0));
-        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-          __builtin_amdgcn_s_sleep(1);
-        SGLM_STAMP(3);
-        if (!(SGLM_DBG(a) & 1)) row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
-      }
-    }
-    SGLM_STAMP(4);
-    if constexpr (row_wave && T::NT > 0)  // the row waves' tiles, after the row stage
-      if (has_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
-    SGLM_STAMP(5);
-    lds_barrier();
-    SGLM_STAMP(6);
-    if (row_wave && blk >= b0 && blk + 2 < b1 && !(SGLM_DBG(a) & 4)) stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
-    SGLM_STAMP(7);
-  };
-  if (b0 < b1) iteration(b0 - 1, std::false_type{});
-#pragma unroll 1
-  for (int64_t blk = b0; blk < b1; ++blk) iteration(blk, std::true_type{});
-#endif
   if (row_wave) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue: this workgroup's partial (the layout of K1's) ----
@@ -1023,7 +869,6 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
       const InitConst ic = init_const(FAM, LNK, a.mode, a.mu0);
       for (int k = 0; k < 6; ++k) lds[R::OFF_INIT + k] = ic.v[k];
     }
-  SGLM_HWID(wv);
   __syncthreads();
   switch (wv) {
     case 0: pass_body_r<P16, FAM, LNK, 0>(lds, a, lane); break;
@@ -1271,12 +1116,10 @@ static void launch_pass_r(const PassArgs& a, int grid, hipStream_t st) {
 }
 
 // K1r runs column-block counts P16 >= the threshold PassArgs::fused_split carries (1: the default
-// SGLM_K1R_MIN_P16, 0: never) -- one 12-wave workgroup per CU; K1 the rest.
-#ifndef SGLM_K1R_MIN_P16
-#define SGLM_K1R_MIN_P16 10
-#endif
+// K1R_MIN_P16, 0: never) -- one 12-wave workgroup per CU; K1 the rest.
+constexpr int K1R_MIN_P16 = 10;
 bool pass_uses_split(int P16, int fused_split, int64_t ld) {
-  const int thr = fused_split == 1 ? SGLM_K1R_MIN_P16 : fused_split;
+  const int thr = fused_split == 1 ? K1R_MIN_P16 : fused_split;
   return fused_split != 0 && P16 >= 6 && P16 >= thr && ld * 24 + 4096 < ((int64_t)1 << 32);
 }
 

@@ -34,24 +34,6 @@
 #include "kernels.hpp"
 #include "rowmath.hpp"
 
-#ifdef SGLM_STAMPS
-// Diagnostic build only (tools/stamps.py NARROW=1): per-phase s_memtime stamps of workgroup
-// 0's waves over 16 steady-state blocks.  [wave 8][block 16][event 8]
-__device__ unsigned long long sglm_nstamp_buf[8 * 16 * 8];
-#define NSTAMP(ev)                                                                                  \
-  do {                                                                                              \
-    if (blockIdx.x == 0 && blk >= b0 + 100 && blk < b0 + 116 && lane == 0)                          \
-      sglm_nstamp_buf[(wv * 16 + (int)(blk - b0 - 100)) * 8 + (ev)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-extern "C" int sglm_debug_nstamps(unsigned long long* out, long count) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sglm_nstamp_buf), sizeof(unsigned long long) * count);
-}
-#else
-#define NSTAMP(ev) \
-  do {             \
-  } while (0)
-#endif
-
 namespace sglm {
 
 namespace {
@@ -59,34 +41,11 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-#ifndef SGLM_NPRIO
-#define SGLM_NPRIO 4
-#endif
-// Diagonal 16x16 tiles on v_mfma_f64_4x4x4f64 (4 blocks): three MFMAs of 16 cycles cover the
-// 10 lower 4x4 sub-blocks of a symmetric tile (B operand rotated by 0, 4, 8 lanes within each
-// 16-lane row, read from LDS at the rotated column) instead of one 64-cycle 16x16x4 that also
-// computes the upper half.  Measured (tools/ab_narrow2.sh, round 2): correct, but p = 32
-// +1 % and p = 64 +39 % per pass -- the 4x4x4 accumulation chains and the extra rotated-operand
-// LDS reads cost more than the 25 % of diagonal-tile MFMA cycles they save.  Off by default.
-// SGLM_NDIAG44 = 2: the same in the row-pair loop only (p <= 32), with the rotated B operands
-// formed from the registers by DPP row rotations instead of LDS reads.
-#ifndef SGLM_NDIAG44
-#define SGLM_NDIAG44 0
-#endif
-// Batched Gram phase (all operands, then all VALU, then all MFMAs per block); 0 selects the
-// per-k-step loop for A/B comparisons (tools/ab_narrow.sh).
-#ifndef SGLM_NBATCH
-#define SGLM_NBATCH 0
-#endif
-// Row pairs (NRB = 32, p <= 32): the family arithmetic runs on 32 of the wave's 64 lanes, so
-// blocks are taken in pairs -- the first block's eta, row values and Gram operands are stashed
-// in registers and its buffer released at once; with the second block, the family arithmetic
-// covers both blocks' rows on all 64 lanes (upper half: the stashed block), then both blocks'
-// MFMAs run from registers.  Half the family-arithmetic instructions per row.
-#ifndef SGLM_NPAIR
-#define SGLM_NPAIR 1
-#endif
-constexpr int NPRIO = SGLM_NPRIO;
+// Issue priority of the two waves of a SIMD alternates every NPRIO blocks (2 / 8 / 16 measured
+// equal or slower).  Measured and not kept (DESIGN.md 4 K1'): the diagonal tiles on three
+// v_mfma_f64_4x4x4f64 (rotated B operands from LDS or by DPP: slower at p = 32 and 64); a
+// batched Gram phase (all operands, then all VALU, then all MFMAs per block: p = 64 +25 %).
+constexpr int NPRIO = 4;
 
 // Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
 // (LDS: 8 waves x 2 buffers).  Row swizzle f(c): 2((c >> 1) & 7) at NRB = 16 (the column
@@ -117,8 +76,12 @@ struct NGeo {
   static constexpr int XB = P16 * BSTR;              // doubles of X per buffer
   static constexpr int BUF = XB + 4 * NRB;           // + y, m, offset, prior
   static constexpr int OFF_W = 2 * BUF;              // w[NRB], w*z[NRB] (PAIR: w[2 NRB], w*z[2 NRB])
-  static constexpr bool PAIR = SGLM_NPAIR && NRB == 32;
-  static constexpr bool D44 = PAIR ? SGLM_NDIAG44 != 0 : SGLM_NDIAG44 == 1;  // diagonal tiles on 4x4x4
+  // Row pairs (NRB = 32, p <= 32): the family arithmetic runs on 32 of the wave's 64 lanes, so
+  // blocks are taken in pairs -- the first block's eta, row values and Gram operands are stashed
+  // in registers and its buffer released at once; with the second block, the family arithmetic
+  // covers both blocks' rows on all 64 lanes (upper half: the stashed block), then both blocks'
+  // MFMAs run from registers.  Half the family-arithmetic instructions per row.
+  static constexpr bool PAIR = NRB == 32;
   static constexpr int WAVE_LDS = OFF_W + (PAIR ? 4 : 2) * NRB;  // doubles per wave
   static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
@@ -147,16 +110,6 @@ __device__ __forceinline__ double xor32_sum(double v) {
   return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
 }
 
-// v within each 16-lane row rotated so that lane 16 q + c reads lane 16 q + ((c + R) & 15):
-// DPP row_ror:(16 - R) on both halves of the double.
-template <int R>
-__device__ __forceinline__ double row_rot(double v) {
-  constexpr int ctrl = 0x120 + ((16 - R) & 15);  // row_ror
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
 // DMA of block blk into buffer buf of this wave's image: NOCT wave-instructions of CPI
 // columns x NRB rows (1 KiB each) + one for the block's slices of y, m, offset, prior
 // (4 x NRB doubles on 2 NRB lanes).  Column groups past the stored columns re-load the last
@@ -179,27 +132,14 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
     __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
 }
 
-// One k-step (4 rows) of the lower-triangular Gram: off-diagonal tiles on 16x16x4; diagonal
-// tiles on 16x16x4 or (SGLM_NDIAG44) on three 4x4x4 MFMAs into acc[t][0..2]: with A = w x of
-// the tile's columns (lane 16k + 4 blk + m: row k, column 4 blk + m -- the 16x16x4 A layout),
-// the B operand rotated by rr groups of 4 lanes (column 4 ((blk + rr) & 3) + n) gives block blk
-// the 4x4 sub-block (blk, (blk + rr) & 3) of the tile in lane 16 m + 4 blk + n.
-template <int P16, bool D44 = NGeo<P16>::D44>
-__device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double (&av)[P16], const double (&xv)[P16],
-                                           const double (&x1)[P16], const double (&x2)[P16]) {
+// One k-step (4 rows) of the lower-triangular Gram on v_mfma_f64_16x16x4_f64.
+template <int P16>
+__device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double (&av)[P16], const double (&xv)[P16]) {
   int t = 0;
 #pragma unroll
   for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
-    for (int bj = 0; bj <= bi; ++bj, ++t) {
-      if (D44 && bi == bj) {
-        acc[t][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], xv[bi], acc[t][0], 0, 0, 0);
-        acc[t][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x1[bi], acc[t][1], 0, 0, 0);
-        acc[t][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[bi], x2[bi], acc[t][2], 0, 0, 0);
-      } else {
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
-      }
-    }
+    for (int bj = 0; bj <= bi; ++bj, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
 }
 
 // IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
@@ -284,11 +224,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 
   const int cl = lane & 15, rq = lane >> 4;
   const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
-  // diagonal-tile B operands rotated by 4 and 8 columns within the 16-column block
-  const int cl1 = (cl + 4) & 15, cl2 = (cl + 8) & 15;
-  const int off1 = cl1 * NRB - cl * NRB, off2 = cl2 * NRB - cl * NRB;
-  const int fc1 = swz<NRB>(cl1), fc2 = swz<NRB>(cl2);
-  const bool do_rows = !(SGLM_DBG(a) & 1), do_gram = !(SGLM_DBG(a) & 2) && !a.no_gram, do_dma = !(SGLM_DBG(a) & 4);
+  const bool do_gram = !a.no_gram;
 
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
   if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
@@ -317,7 +253,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       const double* xs = wl + buf * G::BUF;
       const double* vv = xs + G::XB;
       double eta = 0.0;
-      if (irls && !(SGLM_DBG(a) & 8)) {
+      if (irls) {
         double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
@@ -344,7 +280,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
           for (int b = 0; b < P16; ++b) xp[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+        if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
         continue;
       }
       // family arithmetic: lanes [0, 32) this block's row rl, lanes [32, 64) the stashed block's
@@ -354,10 +290,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       if (!(single && hi)) {
         const double et = hi ? eta_p : eta;
         if (irls && has_eta) a.eta_out[row] = et;
-        if (row < a.n && do_rows) {
+        if (row < a.n) {
           const double y = hi ? y_p : yv, m = hi ? m_p : mv, off = hi ? off_p : ov, pw = hi ? pw_p : pv;
-          if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = et * w; s_dev += w; }
-          else if constexpr (STATS)
+          if constexpr (STATS)
             pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
           else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
@@ -380,7 +315,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
         for (int b = 0; b < P16; ++b) xc[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+      if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
       if (do_gram) {
         // rows in order: the stashed block (upper-half w), then this one
 #pragma unroll
@@ -390,18 +325,14 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           for (int k = 0; k < KS; ++k) {
             const int r = 4 * k + rq + (h == 0 ? NRB : 0);
             const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + 2 * NRB + r];
-            double av[P16], xk[P16], d1[P16], d2[P16];
+            double av[P16], xk[P16];
 #pragma unroll
             for (int b = 0; b < P16; ++b) {
               xk[b] = h == 0 ? xp[k][b] : xc[k][b];
               av[b] = xk[b] * wr;
               xz[b] += xk[b] * wzr;
-              if constexpr (G::D44) {  // columns 4 and 8 on within the 16-column block
-                d1[b] = row_rot<4>(xk[b]);
-                d2[b] = row_rot<8>(xk[b]);
-              }
             }
-            gram_kstep<P16>(acc, av, xk, d1, d2);
+            gram_kstep<P16>(acc, av, xk);
           }
         }
       }
@@ -417,17 +348,15 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
-    NSTAMP(0);
     // block blk landed; block blk+1 (and the previous block's eta store) may still fly
     if (blk + 1 >= b1) wait_vm<0>();
     else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
     else wait_vm<G::NOCT + 1>();
-    NSTAMP(1);
     const double* xs = wl + buf * G::BUF;
 
     // ---- row stage ----
     double eta = 0.0;
-    if (irls && !(SGLM_DBG(a) & 8)) {
+    if (irls) {
       double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int u = 0; u < CPL; ++u) {
@@ -446,13 +375,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         eta = eta + (a.off ? vv[2 * NRB + rl] : 0.0);
         if (has_eta) a.eta_out[row] = eta;  // always issued (row < n_pad): keeps vmcnt exact
       }
-      if (row < a.n && do_rows) {
+      if (row < a.n) {
         const double y = vv[rl];
         const double m = a.m ? vv[NRB + rl] : 1.0;
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
-        if (SGLM_DBG(a) & 16) { w = y * 0.25; wz = eta * w; s_dev += w; }
-        else if constexpr (STATS)
+        if constexpr (STATS)
           pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
         else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
@@ -468,145 +396,27 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       wl[G::OFF_W + NRB + rl] = wz;
     }
 
-    NSTAMP(2);
-#if SGLM_NBATCH
-    // ---- Gramian, batched: every operand of the block's NRB/4 k-steps is read into registers,
-    // the LDS buffer is released to the next DMA at once, then the VALU scaling (A = w x) and
-    // X'Wz, then all T * NRB/4 MFMAs back to back.  fp64 VALU and MFMA share the SIMD's DP
-    // pipe (tools/coexec_bench.hip: they serialise), so the per-k-step VALU -> MFMA -> VALU
-    // alternation of the unbatched loop left a dependency bubble at every switch.
-    {
-      constexpr int KS = NRB / 4;
-      double xv[KS][P16], av[KS][P16], wr[KS], wzr[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int r = 4 * s + rq;
-        const double* base = xs + cl * NRB + (r ^ fcl);
-#pragma unroll
-        for (int b = 0; b < P16; ++b) xv[s][b] = base[G::BSTR * b];
-        wr[s] = wl[G::OFF_W + r];
-        wzr[s] = wl[G::OFF_W + NRB + r];
-      }
-      // every LDS read of this buffer has returned: the DMA of block blk + 2 may overwrite it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      NSTAMP(3);
-      if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
-      NSTAMP(4);
-      if (do_gram) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int b = 0; b < P16; ++b) {
-            av[s][b] = xv[s][b] * wr[s];
-            xz[b] += xv[s][b] * wzr[s];
-          }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          int t = 0;
-#pragma unroll
-          for (int bi = 0; bi < P16; ++bi)
-#pragma unroll
-            for (int bj = 0; bj <= bi; ++bj, ++t)
-              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s][bi], xv[s][bj], acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-#else
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
-    if (do_gram && P16 > 2) {
+    if (do_gram) {  // (p > 32 here: p <= 32 takes the row-pair loop above)
 #pragma unroll
       for (int s = 0; s < NRB / 4; ++s) {
         const int r = 4 * s + rq;
         const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + NRB + r];
         const double* base = xs + cl * NRB + (r ^ fcl);
-        const double* base1 = xs + cl * NRB + off1 + (r ^ fc1);
-        const double* base2 = xs + cl * NRB + off2 + (r ^ fc2);
-        double xv[P16], av[P16], x1[P16], x2[P16];
+        double xv[P16], av[P16];
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
           xv[b] = base[G::BSTR * b];
-          if (G::D44) {
-            x1[b] = base1[G::BSTR * b];
-            x2[b] = base2[G::BSTR * b];
-          }
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
-        gram_kstep<P16>(acc, av, xv, x1, x2);
-      }
-    }
-    if (do_gram && P16 <= 2) {
-      // p <= 32 (3 MFMAs per k-step): software-pipelined -- k-step s+1's operands are read from
-      // LDS before k-step s's MFMAs issue, so their latency hides under the MFMA pipe.  (At
-      // p > 32, 10 MFMAs per k-step already cover it; measured +1.4 % there, mean of 5, not kept.)
-      double xv[P16], x1[P16], x2[P16], wr, wzr;
-      {
-        const double* base = xs + cl * NRB + (rq ^ fcl);
-        const double* base1 = xs + cl * NRB + off1 + (rq ^ fc1);
-        const double* base2 = xs + cl * NRB + off2 + (rq ^ fc2);
-        wr = wl[G::OFF_W + rq];
-        wzr = wl[G::OFF_W + NRB + rq];
-#pragma unroll
-        for (int b = 0; b < P16; ++b) {
-          xv[b] = base[G::BSTR * b];
-          if (G::D44) {
-            x1[b] = base1[G::BSTR * b];
-            x2[b] = base2[G::BSTR * b];
-          }
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < NRB / 4; ++s) {
-        double xn[P16], xn1[P16], xn2[P16], wrn = 0.0, wzrn = 0.0;
-        if (s + 1 < NRB / 4) {
-          const int r = 4 * (s + 1) + rq;
-          const double* base = xs + cl * NRB + (r ^ fcl);
-          const double* base1 = xs + cl * NRB + off1 + (r ^ fc1);
-          const double* base2 = xs + cl * NRB + off2 + (r ^ fc2);
-          wrn = wl[G::OFF_W + r];
-          wzrn = wl[G::OFF_W + NRB + r];
-#pragma unroll
-          for (int b = 0; b < P16; ++b) {
-            xn[b] = base[G::BSTR * b];
-            if (G::D44) {
-              xn1[b] = base1[G::BSTR * b];
-              xn2[b] = base2[G::BSTR * b];
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        double av[P16];
-#pragma unroll
-        for (int b = 0; b < P16; ++b) {
-          av[b] = xv[b] * wr;
-          xz[b] += xv[b] * wzr;
-        }
-        gram_kstep<P16>(acc, av, xv, x1, x2);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 < NRB / 4) {
-#pragma unroll
-          for (int b = 0; b < P16; ++b) {
-            xv[b] = xn[b];
-            if (G::D44) {
-              x1[b] = xn1[b];
-              x2[b] = xn2[b];
-            }
-          }
-          wr = wrn;
-          wzr = wzrn;
-        }
+        gram_kstep<P16>(acc, av, xv);
       }
     }
     // every LDS read of this buffer has returned before the DMA may overwrite it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    NSTAMP(3);
-    if (blk + 2 < b1 && do_dma) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
-    NSTAMP(4);
+    if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
   }
-#endif
   }  // !PAIR
 
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
@@ -675,22 +485,8 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
       for (int bj = 0; bj <= bi; ++bj, ++t) {
-        if (G::D44 && bi == bj) {
-          // 4x4x4 layout -> tile element (i, j) at 16 i + j (reduce_partials_kernel reads i >= j):
-          // rotation rr, lane 16 m + 4 blk + n holds sub-block (blk, J = (blk + rr) & 3), element
-          // (4 blk + m, 4 J + n); an upper sub-block (blk < J) is stored transposed (the tile is
-          // symmetric), rotation 2's two upper sub-blocks duplicate lower ones and are dropped
-          const int m = lane >> 4, blk = (lane >> 2) & 3, n = lane & 3;
 #pragma unroll
-          for (int rr = 0; rr < 3; ++rr) {
-            const int J = (blk + rr) & 3, i = 4 * blk + m, j = 4 * J + n;
-            if (rr == 0 || blk > J) out[t * 256 + 16 * i + j] = acc[t][rr];
-            else if (rr == 1) out[t * 256 + 16 * j + i] = acc[t][rr];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t][j];
-        }
+        for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[t][j];
       }
     if (lane < 16) {
 #pragma unroll

@@ -14,10 +14,6 @@
 
 #include "common.hpp"
 
-#ifndef SGLM_ESTRIN
-#define SGLM_ESTRIN 0  // 0: Horner forms of exp_small / log_pos (A/B builds)
-#endif
-
 namespace sglm {
 
 // Breeze Gaussian(0,1) as used by the probit link.
@@ -63,16 +59,7 @@ __device__ __forceinline__ double log_pos(double x) {
   const double f = m - 1.0;
   const double s = f * rcp_pos(m + 1.0);
   const double z = s * s;
-#if SGLM_ESTRIN
-  // the same polynomial in Estrin's scheme: dependency depth 4 instead of 9 (the row stage is
-  // latency-bound beside the partner wave's MFMAs on the shared fp64 pipe)
-  const double z2 = z * z;
-  const double a0 = fma(sc(1.0 / 5.0), z, sc(1.0 / 3.0)), a1 = fma(sc(1.0 / 9.0), z, sc(1.0 / 7.0));
-  const double a2 = fma(sc(1.0 / 13.0), z, sc(1.0 / 11.0)), a3 = fma(sc(1.0 / 17.0), z, sc(1.0 / 15.0));
-  const double z4 = z2 * z2;
-  const double b0 = fma(a1, z2, a0), b1 = fma(a3, z2, a2);
-  const double q = fma(fma(sc(1.0 / 19.0), z4, b1), z4, b0);
-#else
+  // (Horner: Estrin's scheme, dependency depth 4 instead of 9, measured +-0 -- not kept)
   double q = sc(1.0 / 19.0);
   q = fma(q, z, sc(1.0 / 17.0));
   q = fma(q, z, sc(1.0 / 15.0));
@@ -82,7 +69,6 @@ __device__ __forceinline__ double log_pos(double x) {
   q = fma(q, z, sc(1.0 / 7.0));
   q = fma(q, z, sc(1.0 / 5.0));
   q = fma(q, z, sc(1.0 / 3.0));
-#endif
   const double lm = fma(2.0 * s, z * q, 2.0 * s);
   const double kd = (double)k;
   return fma(kd, sc(6.93147180559945286227e-01), fma(kd, sc(2.31904681384629955842e-17), lm));
@@ -95,20 +81,6 @@ __device__ __forceinline__ double exp_small(double x) {
   const double kf = rint(x * sc(1.44269504088896338700));
   double r = fma(-kf, sc(6.93147180559945286227e-01), x);
   r = fma(-kf, sc(2.31904681384629955842e-17), r);
-#if SGLM_ESTRIN
-  // Estrin's scheme (depth 5 instead of 13; see log_pos)
-  const double r2 = r * r;
-  const double a0 = r + 1.0, a1 = fma(sc(1.0 / 6.0), r, 0.5);
-  const double a2 = fma(sc(1.0 / 120.0), r, sc(1.0 / 24.0)), a3 = fma(sc(1.0 / 5040.0), r, sc(1.0 / 720.0));
-  const double a4 = fma(sc(1.0 / 362880.0), r, sc(1.0 / 40320.0));
-  const double a5 = fma(sc(1.0 / 39916800.0), r, sc(1.0 / 3628800.0));
-  const double a6 = fma(sc(1.0 / 6227020800.0), r, sc(1.0 / 479001600.0));
-  const double r4 = r2 * r2;
-  const double b0 = fma(a1, r2, a0), b1 = fma(a3, r2, a2), b2 = fma(a5, r2, a4);
-  const double r8 = r4 * r4;
-  const double d0 = fma(b1, r4, b0), d1 = fma(a6, r4, b2);
-  const double q = fma(d1, r8, d0);
-#else
   double q = sc(1.0 / 6227020800.0);  // 1/13!
   q = fma(q, r, sc(1.0 / 479001600.0));
   q = fma(q, r, sc(1.0 / 39916800.0));
@@ -123,7 +95,6 @@ __device__ __forceinline__ double exp_small(double x) {
   q = fma(q, r, 0.5);
   q = fma(q, r, 1.0);
   q = fma(q, r, 1.0);
-#endif
   return __builtin_amdgcn_ldexp(q, (int)kf);
 }
 

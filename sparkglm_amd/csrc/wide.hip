@@ -26,19 +26,6 @@
 #include "procx.hpp"
 #include "rowmath.hpp"
 
-#ifndef WIDE_SPREAD_DMA
-#define WIDE_SPREAD_DMA 1
-#endif
-// Workgroups per CU of the diagonal-super-tile kernel.  Its LDS image is one panel per buffer
-// (33.5 KB), so three fit beside each other; measured (tools/ab_wide.sh): three waves per SIMD
-// instead of two change nothing (p = 512 -0.3 %) and spill a few VGPRs, so two.
-#ifndef WIDE_DIAG_WG
-#define WIDE_DIAG_WG 2
-#endif
-#ifndef WIDE_DIAG_BATCH
-#define WIDE_DIAG_BATCH 0  // diagonal k-steps: operands and VALU of the whole block before its MFMAs
-#endif
-
 namespace sglm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -80,6 +67,10 @@ constexpr int LDS_DOUBLES = OFF_V + 4 * WRB;
 constexpr int OFF_VD = 2 * PB;
 constexpr int LDS_DIAG = OFF_VD + 4 * WRB;
 constexpr int NWAVE = 4;                   // one wave per SIMD; two workgroups per CU
+// Workgroups per CU of the diagonal-super-tile kernel.  Its LDS image is one panel per buffer
+// (33.5 KB), so three fit beside each other; measured: three waves per SIMD instead of two change
+// nothing (p = 512 -0.3 %) and spill a few VGPRs, so two.
+constexpr int DIAG_WG = 2;
 
 __device__ __forceinline__ int swz(int c) { return 2 * ((c >> 1) & 7); }
 
@@ -210,31 +201,7 @@ __device__ __forceinline__ void diag_block(const double* lds, int buf, int lane,
   const double* xs = lds + buf * PB + cl * WRB;
   const double* w = lds + OFF_VD + (buf * 2 + 0) * WRB;
   const double* wz = lds + OFF_VD + (buf * 2 + 1) * WRB;
-#if WIDE_DIAG_BATCH
-  // every operand of the block's 4 k-steps first, the VALU scaling, then 36 MFMAs back to back
-  double xb[WRB / 4][HI + 1], al[WRB / 4], ah[WRB / 4];
-#pragma unroll
-  for (int s = 0; s < WRB / 4; ++s) {
-    const int r = 4 * s + rq;
-    const int o = r ^ f;
-    const double wr = w[r], wzr = wz[r];
-#pragma unroll
-    for (int c = 0; c <= HI; ++c) xb[s][c] = xs[o + TB * c];
-    al[s] = xb[s][LO] * wr;
-    ah[s] = xb[s][HI] * wr;
-    xz_lo += xb[s][LO] * wzr;
-    xz_hi += xb[s][HI] * wzr;
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int s = 0; s < WRB / 4; ++s)
-#pragma unroll
-    for (int k = 0; k <= PT; ++k)
-      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? al[s] : ah[s], xb[s][k <= LO ? k : k - LO - 1], acc[k], 0,
-                                                    0, 0);
-  return;
-#endif
-  // operands of k-step s + 1 are read from LDS while the 9 MFMAs of step s issue
+  // operands of k-step s + 1 (all operands of a block first, then its 36 MFMAs: +0.6 %, not kept) are read from LDS while the 9 MFMAs of step s issue
   double xv[2][HI + 1], wr[2], wzr[2];
   auto load = [&](int s, int slot) {
     const int r = 4 * s + rq;
@@ -307,7 +274,6 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   d4 acc[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
-  const int dbg = SGLM_DBG(a);
   int64_t loff[2];
   lane_offsets(a, lane, loff);
   if (b0 < b1) wstage<false, PROC>(lds, 0, a, b0, I, J, wv, loff, lane);
@@ -316,8 +282,8 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
   for (int64_t blk = b0; blk < b1; blk += bs, cur ^= 1) {
     const int64_t nb = blk + bs;
     wait_vm<0>();
-    if (!(dbg & 32)) lds_bar();
-    const bool next = nb < b1 && (!(dbg & 4) || blk == b0);
+    lds_bar();
+    const bool next = nb < b1;
     if constexpr (PROC) {  // generate block blk+1 two octets per k-step, under the MFMAs
       offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
         if (!next) return;
@@ -326,7 +292,7 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
         if (s == 2) wstage<false, true, 4, 6>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
         if (s == 3) wstage<false, true, 6, 8>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
       });
-    } else if (WIDE_SPREAD_DMA) {  // issue block blk+1's DMA two octets per k-step, under the MFMAs
+    } else {  // issue block blk+1's DMA two octets per k-step, under the MFMAs
       offdiag_block(lds, cur, wv, lane, acc, [&](int s) {
         if (!next) return;
         if (s == 0) wstage<false, false, 0, 2>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
@@ -334,9 +300,6 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
         if (s == 2) wstage<false, false, 4, 6>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
         if (s == 3) wstage<false, false, 6, 8>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
       });
-    } else {
-      if (next) wstage<false, false>(lds, cur ^ 1, a, nb, I, J, wv, loff, lane);
-      offdiag_block(lds, cur, wv, lane, acc, [](int) {});
     }
   }
   const int tr0 = 4 * (wv >> 1), tc0 = 4 * (wv & 1);
@@ -356,7 +319,7 @@ __device__ void offdiag_piece(double* lds, const WideGramArgs& a, int I, int J, 
 // each gets the whole register file): workgroup g runs the pieces [wg_begin[g],
 // wg_begin[g+1]) of the cost-balanced schedule built on the host (engine.cpp).
 template <bool DIAG, bool PROC>
-__global__ void __launch_bounds__(64 * NWAVE, DIAG ? WIDE_DIAG_WG : 2) wide_gram_kernel(WideGramArgs a) {
+__global__ void __launch_bounds__(64 * NWAVE, DIAG ? DIAG_WG : 2) wide_gram_kernel(WideGramArgs a) {
   __shared__ double lds[DIAG ? LDS_DIAG : LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -515,24 +478,18 @@ __device__ __forceinline__ void wide_rows_body(const WideRowArgs& a) {
   }
 }
 
-#ifndef SGLM_WIDE_RPT
-#define SGLM_WIDE_RPT 4
-#endif
-#ifndef WIDE_ROW_NT
-#define WIDE_ROW_NT 1  // overlapped row kernel: non-temporal X loads (keep the Gram's rows in the caches)
-#endif
 template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
-  wide_rows_body<FAM, LNK, SGLM_WIDE_RPT>(a);
+  wide_rows_body<FAM, LNK, 4>(a);
 }
 
 // The same row stage for the overlapped chunks (engine.cpp enqueue_pass): one workgroup per CU
 // beside the two persistent Gram workgroups, so at most 96 VGPRs (2 x 208 + 96 = the SIMD's
 // 512) and two rows per thread (no spills at that budget).  Per-row arithmetic and order are the
-// full kernel's, bit for bit.
+// full kernel's, bit for bit.  Non-temporal X loads keep the Gram's rows in the caches.
 template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) wide_rows_ov_kernel(WideRowArgs a) {
-  wide_rows_body<FAM, LNK, 2, WIDE_ROW_NT != 0>(a);
+  wide_rows_body<FAM, LNK, 2, true>(a);
 }
 
 // Packed output: lower-tri X'WX row-major | X'Wz | NS scalars, summed in a fixed order.
@@ -670,7 +627,7 @@ hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st, bool
             : launch_rows_fl<wide_rows_kernel_t>(fam, lnk, g, b, st, a);
 }
 
-int wide_gram_wg_per_cu(bool diag) { return diag ? WIDE_DIAG_WG : 2; }
+int wide_gram_wg_per_cu(bool diag) { return diag ? DIAG_WG : 2; }
 
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st) {
   if (diag && a.proc.on)

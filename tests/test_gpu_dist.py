@@ -1,6 +1,9 @@
-"""Multi-rank GPU paths on one MI355X: two rank processes sharing the device with the
-engine's host all-reduce over gloo, the native RCCL communicator, and torch's RCCL
-("nccl") group through the device-buffer callback."""
+"""Multi-rank GPU paths on one MI355X: rank processes sharing the device with the engine's
+host all-reduce over gloo, the native RCCL communicator, torch's RCCL ("nccl") group through
+the device-buffer callback -- and, at world 2 and 4, the DEVICE-buffer all-reduce path
+(stage_rank_block + the rank blocks of the packed buffer in HBM, engine.cpp) over a gloo group
+of CUDA tensors: the buffers and the staging an RCCL communicator carries across GPUs, exercised
+with several ranks before an 8-GPU node runs them (utils.scala:110-126, GLM.scala:404-407)."""
 import os
 import socket
 import sys
@@ -39,13 +42,18 @@ def _worker(rank, world, port, mode, q):
         uid = [Engine.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.set_comm_rccl(world, rank, uid[0])
+    elif mode == "gloo-device":  # device buffers through a gloo group of CUDA tensors
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        eng.set_comm(D.torch_allreduce(), on_device=True, rank=rank)
     else:  # torch nccl group, device buffers
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         eng.set_comm(D.torch_allreduce(), on_device=True, rank=rank)
     f = eng.fit_glm("poisson", "log", init="multiple")
+    st = eng.stats()
     q.put((rank, (f.coefs, f.stderr, np.array([f.deviance, f.null_deviance, f.pearson, f.loglik, f.iter, f.nrow,
-                                                f.npart]))))
+                                                f.npart]), (st["comm_path_name"], st["rank_blocks"]))))
     dist.barrier()
     eng.close()
     dist.destroy_process_group()
@@ -65,20 +73,27 @@ def _run(mode, world):
     return res
 
 
-def _reference():
+def _reference(world):
+    """fitMultipleBinomial over `world` row partitions (the partitioned oracle)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
     from sparkglm_amd import synth
     X, y, off, pr = synth.generate(2, 0, 40_000, 48, 5)
-    return po.fit_glm(X, y, "poisson", "log", offset=off, prior=pr, npart=2, nthreads=2)
+    return po.fit_glm(X, y, "poisson", "log", offset=off, prior=pr, npart=max(world, 2), nthreads=2)
 
 
-@pytest.mark.parametrize("mode,world", [("gloo", 2), ("rccl", 1), ("nccl", 1)])
+PATH = {"gloo": "caller-host", "gloo-device": "caller-device", "rccl": "rccl", "nccl": "caller-device"}
+
+
+@pytest.mark.parametrize("mode,world", [("gloo", 2), ("rccl", 1), ("nccl", 1), ("gloo-device", 2),
+                                        ("gloo-device", 4)])
 def test_sharded_fit_equals_oracle(mode, world):
     res = _run(mode, world)
-    ref = _reference()
+    ref = _reference(world)
     for r in range(world):
-        coefs, se, s = res[r]
+        coefs, se, s, (path, blocks) = res[r]
+        assert path == PATH[mode], path
+        assert blocks == (1 if world > 1 else 0)  # the scalars through the rank blocks of the buffer
         assert int(s[4]) == ref.iter and s[5] == 40_000 and int(s[6]) == world
         assert rel(coefs, ref.coefs) < 1e-9 and rel(se, ref.stderr) < 1e-9
         assert rel(s[:4], [ref.deviance, ref.null_deviance, ref.pearson, ref.loglik]) < 1e-9

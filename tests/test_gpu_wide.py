@@ -280,3 +280,22 @@ def test_wide_singular_gram_raises_matrix_singular(weng):
     weng.set_data(X, y)
     with pytest.raises(L.MatrixSingularException):
         weng.fit_lm()
+
+
+@pytest.mark.parametrize("kind,p,fam,link", [(0, 300, "binomial", "logit"), (3, 520, "gamma", "inverse")])
+def test_procedural_in_kernel_generation_is_bitwise_the_chunked_fit(kind, p, fam, link):
+    """SGLM_PROC_CHUNKS=0 selects the procedural path's fallback for too little free HBM: the Gram
+    kernels regenerate every X octet they stage (wide_gram_kernel<..., PROC = true>) instead of
+    reading a generated chunk -- the same values in the same order, so the same fit bit for bit."""
+    n, row0 = 5000, 4321
+    with Engine(0) as e:
+        e.synth(kind, row0, n, p, 8, procedural=True)
+        assert e.stats()["proc_chunks"] >= 1
+        a = e.fit_glm(fam, link)
+    with _engine_env(SGLM_PROC_CHUNKS="0") as e:
+        e.synth(kind, row0, n, p, 8, procedural=True)
+        assert e.stats()["proc_chunks"] == 0
+        b = e.fit_glm(fam, link)
+    np.testing.assert_array_equal(a.coefs, b.coefs)
+    np.testing.assert_array_equal(a.stderr, b.stderr)
+    assert (a.deviance, a.pearson, a.loglik, a.iter) == (b.deviance, b.pearson, b.loglik, b.iter)

@@ -290,21 +290,12 @@ def main() -> int:
         nvec = 1 + (2 if wl["kind"] == 2 else 0)  # y (+ offset, prior)
         flops = n * (p * (p + 1) + 2 * p)      # SYRK-convention X'WX + X'Wz per launch
         bytes_pass = n * (8 * p + 8 * nvec)    # X row + per-row vectors, read once per pass
+        # the kernel is the one the engine dispatched (sglm_stats.pass_kernel_name), not re-derived here
+        kern = st["pass_kernel_name"] + (" (K1r, split-role fused pass)" if st["pass_kernel_kind"] == "fused-split" else "")
         if wide:
-            kern = "wide_gram_kernel"
             kern_ms = st["gram_kernel_ms"] / passes
             pass_ms = st["pass_kernel_ms"] / passes  # wall span of the pass (row and Gram may overlap)
-        elif st["path"] == 2:
-            kern = f"irls_narrow_kernel<{(p + 15) // 16},{fam},{lnk}>"
-            kern_ms = st["pass_kernel_ms"] / passes
-            pass_ms = kern_ms
         else:
-            p16 = (p + 15) // 16 + ((p + 15) // 16) % 2
-            fs = int(os.environ.get("SGLM_FUSED_SPLIT", "1") or 0)  # engine.cpp fused_split, kernels.hip pass_uses_split
-            if fs != 0 and p16 >= max(6, 10 if fs == 1 else fs):  # K1r
-                kern = f"irls_pass_r_kernel<{fam},{lnk}> (K1r, split-role fused pass)"
-            else:
-                kern = f"irls_pass_kernel<{p16},{fam},{lnk}>"
             kern_ms = st["pass_kernel_ms"] / passes
             pass_ms = kern_ms
         tflops = flops / (kern_ms * 1e-3) / 1e12
@@ -561,7 +552,7 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
                        "link": "identity"},
             "time_to_converge_s": dt / args.steps, "iters_to_converge": 1,
             "r2": fit.r2, "sse": fit.sse,
-            "roofline": {"bound": "hbm", "kernel": f"irls_narrow_kernel<{(p + 15) // 16},gaussian,identity> (LM Gram)",
+            "roofline": {"bound": "hbm", "kernel": st["pass_kernel_name"] + " (LM Gram)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                          "traffic": None, "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass,
                          "note": "1M x 20 = 168 MB per pass: launch- and latency-bound, not a bandwidth test"},

@@ -55,9 +55,10 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 5  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
+#define SGLM_ABI_VERSION 6  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
                               sglm_stats.comm_path / rank_blocks / pass_kernel_ms_min / proc_chunks /
-                              proc_chunk_rows / solve_path */
+                              proc_chunk_rows / solve_path; 6: sglm_stats.pass_kernel / pass_kernel_name,
+                              sglm_set_comm_rank collective */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -99,6 +100,16 @@ enum sglm_comm_path {
   SGLM_COMM_RCCL = 3,         /* sglm_set_comm_rccl: the engine's own RCCL communicator (xGMI) */
   SGLM_COMM_GROUP_RCCL = 4,   /* multi-device handle: one RCCL group call over ncclCommInitAll */
   SGLM_COMM_GROUP_HOST = 5    /* multi-device handle with a repeated device: host sums in shard order */
+};
+
+/* The kernel that ran the last pass (sglm_stats.pass_kernel; the roofline line's `kernel`). */
+enum sglm_pass_kernel {
+  SGLM_KERNEL_NONE = 0,
+  SGLM_KERNEL_FUSED = 1,       /* irls_pass_kernel<P16, fam, link>: 65 <= p <= 256 below the K1r threshold */
+  SGLM_KERNEL_FUSED_SPLIT = 2, /* irls_pass_r_kernel<P16, fam, link> (K1r, split roles) */
+  SGLM_KERNEL_NARROW = 3,      /* irls_narrow_kernel<P16, fam, link, irls, stats>: p <= 64 */
+  SGLM_KERNEL_WIDE = 4,        /* wide_rows_kernel + wide_gram_kernel: p > 256 (resident X) */
+  SGLM_KERNEL_WIDE_PROC = 5    /* the same over procedural X (generated chunks or in-kernel) */
 };
 
 /* Prediction scale (R's predict(type = "link" | "response")). */
@@ -178,6 +189,9 @@ typedef struct {
   int proc_chunks;          /* procedural shard: chunks of X generated per pass (0: in-kernel) */
   int64_t proc_chunk_rows;  /* rows per chunk (SGLM_PROC_SCRATCH_MAX caps the scratch, GiB) */
   int solve_path;           /* enum sglm_solve_path of the last solve, -1 before any */
+  int pass_kernel;          /* enum sglm_pass_kernel of the last pass (the engine's own choice: the K1 / K1r
+                               threshold, its row limit, the narrow / wide paths) */
+  char pass_kernel_name[64];/* that kernel's name as rocprofv3 lists it, e.g. "irls_pass_r_kernel<16,binomial,logit>" */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
@@ -235,7 +249,9 @@ int sglm_set_comm(sglm_engine *h, sglm_allreduce_fn fn, void *ctx, int on_device
 /* This handle's rank in the communicator just set by sglm_set_comm (0 <= rank < its rank count;
  * known without this call for RCCL and sglm_local_allreduce).  With it the per-iteration scalars
  * (deviance, Pearson, loglik) are summed across ranks in rank order with compensation, so the
- * convergence test does not depend on the rank count beyond ~1 ulp. */
+ * convergence test does not depend on the rank count beyond ~1 ulp.  COLLECTIVE: every rank of the
+ * communicator calls it (it changes the length of every later all-reduce); one all-reduce checks
+ * that all ranks joined with distinct ranks, else SGLM_EINVAL on every rank. */
 int sglm_set_comm_rank(sglm_engine *h, int rank);
 /* Native RCCL communicator over xGMI.  unique_id: 128 bytes from
  * sglm_rccl_unique_id() on rank 0, broadcast by the caller. */
@@ -279,6 +295,12 @@ int sglm_predict_new(sglm_engine *h, const double *X, int64_t n, int64_t p, int6
                      int type, double *out);
 
 int sglm_get_stats(sglm_engine *h, sglm_stats *out);
+/* The kernel an engine would run a pass of an n x p shard with (enum sglm_pass_kernel, -1 on bad
+ * arguments) and its name into name[namelen] -- the engine's own dispatch rule, for callers and CPU
+ * tests.  fused_split: SGLM_FUSED_SPLIT's meaning (1 default threshold, 0 never K1r, N from P16 = N);
+ * flags: 1 procedural shard, 2 forced wide path (SGLM_FORCE_WIDE).  No device is touched. */
+int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int family, int link, char *name,
+                         int64_t namelen);
 int sglm_reset_stats(sglm_engine *h);
 
 /* ---- external backend: the same IRLS driver over caller-computed partials ---------

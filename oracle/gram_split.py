@@ -100,6 +100,33 @@ def compare(engine_path: str, oracle_path: str) -> dict:
            "c_gram_order_through_lu": {"elementwise_max": rel_elem(x_lu_e, x_lu_o), "normwise": rel_norm(x_lu_e, x_lu_o)},
            "total_engine_vs_oracle_solve": {"elementwise_max": rel_elem(x_chol_e, x_lu_o),
                                             "normwise": rel_norm(x_chol_e, x_lu_o)}}
+    # the reference's own implementation spread on THIS matrix (the oracle's Gram): Breeze inv is LAPACK
+    # dgetrf + dgetri as netlib-java binds it (here OpenBLAS through scipy), the oracle restates it
+    # unblocked; a Cholesky solve is the engine's algorithm; the product inv * b in BLAS order
+    import scipy.linalg as sl
+    lu, piv = sl.lu_factor(Go)
+    Gi_lapack, info = sl.lapack.dgetri(lu, piv)
+    x_lapack = np.zeros(p)
+    for k in range(p):
+        x_lapack = x_lapack + Gi_lapack[:, k] * xo[k]
+    x_chol_o = sl.cho_solve(sl.cho_factor(Go, lower=True), xo)
+    res["reference_spread_on_oracle_gram"] = {
+        "lapack_lu_vs_oracle_lu": {"elementwise_max": rel_elem(x_lapack, x_lu_o), "normwise": rel_norm(x_lapack, x_lu_o)},
+        "lapack_lu_blas_product_vs_oracle_lu": {"elementwise_max": rel_elem(Gi_lapack @ xo, x_lu_o),
+                                                "normwise": rel_norm(Gi_lapack @ xo, x_lu_o)},
+        "lapack_cholesky_vs_oracle_lu": {"elementwise_max": rel_elem(x_chol_o, x_lu_o),
+                                         "normwise": rel_norm(x_chol_o, x_lu_o)}}
+    # the same in units of the solve's backward-error scale per coefficient, cond * eps * max|x| / |x_i|
+    # (tests/test_gpu_configs.py wide_elementwise_ok bounds the engine by K_BOUND of these units)
+    scale = cond * np.finfo(float).eps * np.max(np.abs(x_lu_o)) / np.abs(x_lu_o)
+    res["K_units"] = {"reference_lapack_vs_oracle_lu": float(np.max(np.abs(x_lapack - x_lu_o) / np.abs(x_lu_o) / scale)),
+                      "engine_chol_vs_oracle_lu": float(np.max(np.abs(x_chol_e - x_lu_o) / np.abs(x_lu_o) / scale))}
+    if "fit_coefs" in e:
+        fc = np.asarray(full_scale_case()["coefs"])
+        res["K_units"]["engine_fit_vs_oracle_fit"] = float(np.max(np.abs(e["fit_coefs"] - fc) / np.abs(fc) / scale))
+    if "x_lu_roc" in e:  # the engine's LU route (SGLM_WIDE_SOLVE=lu: rocSOLVER getrf + getri, inv * b in order)
+        res["b_engine_lu_route_vs_oracle_lu_on_engine_gram"] = {"elementwise_max": rel_elem(e["x_lu_roc"], x_lu_e),
+                                                                 "normwise": rel_norm(e["x_lu_roc"], x_lu_e)}
     if "fit_coefs" in e:
         c = full_scale_case()
         res["engine_fit_vs_oracle_fit"] = {"elementwise_max": rel_elem(e["fit_coefs"], c["coefs"]),

@@ -31,7 +31,7 @@ EXPORTS = [
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
     "sglm_pval_normal", "sglm_pval_t", "sglm_create_multi", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
     "sglm_predict_glm", "sglm_predict_new", "sglm_local_comm_create", "sglm_local_comm_destroy",
-    "sglm_local_comm_rank", "sglm_local_allreduce", "sglm_set_comm_rank",
+    "sglm_local_comm_rank", "sglm_local_allreduce", "sglm_set_comm_rank", "sglm_pass_kernel_for",
 ]
 PREDICT_LINK, PREDICT_RESPONSE = 0, 1
 
@@ -63,11 +63,12 @@ class Stats(C.Structure):
                 ("ndev", C.c_int), ("rccl_group", C.c_int), ("dev_passes", C.c_int64),
                 ("overlap_chunks", C.c_int), ("comm_path", C.c_int), ("rank_blocks", C.c_int),
                 ("pass_kernel_ms_min", C.c_double), ("proc_chunks", C.c_int), ("proc_chunk_rows", C.c_int64),
-                ("solve_path", C.c_int)]
+                ("solve_path", C.c_int), ("pass_kernel", C.c_int), ("pass_kernel_name", C.c_char * 64)]
 
 
 COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}
 SOLVE_PATHS = {-1: "none", 0: "host-cholesky", 1: "host-lu", 2: "device-cholesky", 3: "device-lu"}
+PASS_KERNELS = {0: "none", 1: "fused", 2: "fused-split", 3: "narrow", 4: "wide", 5: "wide-procedural"}
 
 
 class GlmDerived(C.Structure):
@@ -160,6 +161,8 @@ def load():
         "sglm_local_comm_destroy": ([C.c_void_p], None),
         "sglm_local_comm_rank": ([C.c_void_p, C.c_int], C.c_void_p),
         "sglm_local_allreduce": ([C.c_void_p, dp, C.c_int64, C.c_void_p, C.c_int], C.c_int),
+        "sglm_pass_kernel_for": ([C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int64],
+                                 C.c_int),
     }
     for name, (args, res) in sig.items():
         if os.environ.get("SGLM_LIB") and not hasattr(lib, name):
@@ -169,6 +172,17 @@ def load():
         f.restype = res
     _lib = lib
     return lib
+
+
+def pass_kernel_for(n: int, p: int, family: str = "binomial", link: str = "logit", fused_split: int = 1,
+                    procedural: bool = False, force_wide: bool = False):
+    """(kind, name) of the kernel an engine runs an n x p pass with (sglm_pass_kernel_for; no GPU)."""
+    buf = C.create_string_buffer(64)
+    k = load().sglm_pass_kernel_for(int(n), int(p), int(fused_split), (1 if procedural else 0) | (2 if force_wide else 0),
+                                    FAMILIES[family], LINKS[link], buf, 64)
+    if k < 0:
+        raise IllegalArgumentException(last_error())
+    return PASS_KERNELS[k], buf.value.decode()
 
 
 def last_error() -> str:

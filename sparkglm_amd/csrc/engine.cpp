@@ -121,6 +121,34 @@ void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_
 
 }  // namespace
 
+// Which kernel a pass runs (enum sglm_pass_kernel) and its name: the dispatch rules of
+// ensure_workspace / launch_pass / launch_narrow / the wide path, in one place (the engine labels
+// its passes with it; sglm_pass_kernel_for exposes it for a CPU test of the mapping).
+namespace {
+int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc, int fused_split, int family,
+                       int link, char* name, size_t len) {
+  static const char* fam[] = {"binomial", "gaussian", "poisson", "gamma"};
+  static const char* lnk[] = {"logit", "probit", "cloglog", "identity", "log", "inverse"};
+  const char* f = (family >= 0 && family < 4) ? fam[family] : "?";
+  const char* l = (link >= 0 && link < 6) ? lnk[link] : "?";
+  int k;
+  if (wide) {
+    k = proc ? SGLM_KERNEL_WIDE_PROC : SGLM_KERNEL_WIDE;
+    std::snprintf(name, len, "wide_gram_kernel<%s>", proc ? "procedural" : "resident");
+  } else if (narrow) {
+    k = SGLM_KERNEL_NARROW;
+    std::snprintf(name, len, "irls_narrow_kernel<%d,%s,%s>", P16, f, l);
+  } else if (pass_uses_split(P16, fused_split, n_pad)) {
+    k = SGLM_KERNEL_FUSED_SPLIT;
+    std::snprintf(name, len, "irls_pass_r_kernel<%d,%s,%s>", P16, f, l);
+  } else {
+    k = SGLM_KERNEL_FUSED;
+    std::snprintf(name, len, "irls_pass_kernel<%d,%s,%s>", P16, f, l);
+  }
+  return k;
+}
+}  // namespace
+
 // ---- in-process communicator: N host threads, one handle each (a JVM driver's thread pool) ----
 // Every rank's call blocks until all N have arrived; the last to arrive sums the N buffers in
 // rank order (deterministic, independent of arrival order) and writes the sum into all of them.
@@ -169,9 +197,7 @@ struct sglm_engine : public Backend {
   bool red_on_device = false;  // dred holds the all-reduced result of the last pass
   bool lp_stats = false;       // the last pass carried the final statistics (PassArgs::stats_in_pass)
   double stats_const = 0.0;    // the fit's initial-pass S_AUX2: constant part of in-pass Poisson / Gamma statistics
-  double dev_const = 0.0;      // the fit's initial-pass S_AUX1 (Poisson): sum pw y log y, the deviance's constant part
-  bool lp_devsplit = false;    // the last pass summed the Poisson deviance without that constant (narrow)
-  int consts_family = -1;      // family whose initial pass produced stats_const / dev_const on this data (-1: none)
+  int consts_family = -1;      // family whose initial pass produced stats_const on this data (-1: none)
   // deviance-only passes (Backend::pass_dev): the next enqueue_pass runs the row stage and the
   // scalar reduction but no Gram -- bitwise the scalars of the full pass.  SGLM_SPECULATE=0 off.
   bool dev_only = false, allow_spec = true;
@@ -224,6 +250,8 @@ struct sglm_engine : public Backend {
   int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
+  int last_kernel = SGLM_KERNEL_NONE;  // the kernel of the last pass (enum sglm_pass_kernel) and its name
+  char last_kernel_name[64] = "";
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
   static constexpr int64_t STAGE_DOUBLES = (int64_t)8 << 20;  // 64 MiB each
   double* hstage[2] = {nullptr, nullptr};
@@ -918,12 +946,6 @@ struct sglm_engine : public Backend {
   }
 
   int pass(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) override {
-    // a narrow Poisson IRLS pass needs its deviance constant from an initial pass on this data (a fit
-    // runs one first; a standalone sglm_irls_pass / sglm_irls_iterations gets one here)
-    if (mode == MODE_IRLS && family == FAM_POISSON && consts_family != FAM_POISSON &&
-        (group() ? subs[0]->narrow : narrow)) {
-      if (int rc = pass(MODE_INIT_SINGLE, nullptr, 1.0, 0.0, family, link, packed)) return rc;
-    }
     if (group()) return group_pass(mode, beta, mu0, ybar, family, link, packed);
     const int64_t plen = packed_len(p), sc = tri_count(p) + p;
     const int R = gather_ranks() ? comm.nranks : 0;  // rank blocks of the scalars (compensated_rank_sum)
@@ -960,22 +982,16 @@ struct sglm_engine : public Backend {
   // later pass that carried the statistics -- R's dpois loglik sum pw (y log mu - mu) minus
   // sum pw lgamma(y + 1); Gamma's S_LL = sum pw log y and S_AUX1 = sum pw log mu = sum pw log y -
   // sum pw log(y eta).  Applied once, on the all-reduced scalars.
-  // Likewise the narrow Poisson passes' deviance lacks its constant part sum pw y log y (pass_row
-  // dev_nolog), summed by the initial pass into S_AUX1 and added back here.
+  // (The statistics ride only in passes of a fit, after its initial pass: enqueue_pass.)
   void finish_scalars(int mode, int family, double* s) {
     if (family != FAM_POISSON && family != FAM_GAMMA) return;
     if (mode == MODE_INIT_SINGLE || mode == MODE_INIT_MULTI) {
       stats_const = s[S_AUX2];
       s[S_AUX2] = 0.0;
-      if (family == FAM_POISSON) {
-        dev_const = s[S_AUX1];
-        s[S_AUX1] = 0.0;
-      }
       consts_family = family;
+      for (sglm_engine* sub : subs) sub->consts_family = family;
       return;
     }
-    if (mode == MODE_IRLS && family == FAM_POISSON && (group() ? subs[0]->lp_devsplit : lp_devsplit))
-      s[S_DEV] += dev_const;
     if (mode != MODE_IRLS || !pass_has_stats()) return;
     if (family == FAM_POISSON) {
       s[S_LL] -= stats_const;
@@ -1051,10 +1067,12 @@ struct sglm_engine : public Backend {
     // pass only, the pass glm_drive predicts to end the fit: at p = 64 their statistics rows cost
     // +14 % per pass (125M x 64 Poisson: 17.4 against 15.3 ms, tools/ab_stats.py; the family
     // arithmetic runs on 16 of 64 lanes there), while the deviance-only pass has no Gram to slow.
+    // (Poisson / Gamma: only after this data's initial pass has summed the statistics' constants.)
     a.stats_in_pass = (narrow && mode == MODE_IRLS && stats_in_pass_family(family, link) &&
-                       !(family == FAM_BINOMIAL && dm) && (family == FAM_BINOMIAL || dev_only)) ? 1 : 0;
+                       !(family == FAM_BINOMIAL && dm) &&
+                       (family == FAM_BINOMIAL || (dev_only && consts_family == family))) ? 1 : 0;
     lp_stats = a.stats_in_pass != 0;
-    lp_devsplit = narrow && mode == MODE_IRLS && family == FAM_POISSON;  // narrow.hip: pass_row dev_nolog
+    note_kernel(mode == MODE_LM_GRAM ? FAM_GAUSSIAN : family, mode == MODE_LM_GRAM ? LNK_IDENTITY : link);
     a.eta_out = (mode == MODE_IRLS && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.fused_split = fused_split;
@@ -1197,6 +1215,14 @@ struct sglm_engine : public Backend {
     }
     HIPCHK(hipEventRecord(ev2, st));
     return SGLM_OK;
+  }
+
+  // The kernel this shard's passes run (sglm_stats.pass_kernel / pass_kernel_name): the engine's
+  // own dispatch decision -- narrow / fused / wide, and K1 against K1r by pass_uses_split with its
+  // row limit -- so a roofline line is labelled by what ran, not by a re-derived threshold.
+  void note_kernel(int family, int link) {
+    last_kernel = pass_kernel_choice(n_pad, P16, narrow, wide, procx.on != 0, fused_split, family, link,
+                                     last_kernel_name, sizeof last_kernel_name);
   }
 
   // ---- multi-device handle: every shard's pass enqueued, then one reduction ----
@@ -1953,6 +1979,22 @@ int sglm_set_comm_rank(sglm_engine* h, int rank) {
     set_error("requirement failed: a communicator joined first (sglm_set_comm), 0 <= rank < its rank count");
     return SGLM_EINVAL;
   }
+  // Collective: with a rank the scalars travel in per-rank blocks, which lengthens every later
+  // all-reduce, so every rank must opt in -- with distinct ranks -- or the ranks would post
+  // collectives of different sizes.  One plain all-reduce of (1, r, r^2, r^3) checks both.
+  HIPCHK(hipSetDevice(h->device));
+  h->comm.rank = -1;
+  const double r = rank;
+  double chk[4] = {1.0, r, r * r, r * r * r};
+  if (int rc = h->allreduce_small(chk, 4)) return rc;
+  const double n = h->comm.nranks;
+  const bool ok = chk[0] == n && chk[1] == n * (n - 1) / 2 && chk[2] == (n - 1) * n * (2 * n - 1) / 6 &&
+                  chk[3] == (n * (n - 1) / 2) * (n * (n - 1) / 2);
+  if (!ok) {
+    set_error("requirement failed: sglm_set_comm_rank must be called by every rank of the communicator, each with "
+              "its own distinct rank in [0, " + std::to_string(h->comm.nranks) + ")");
+    return SGLM_EINVAL;
+  }
   h->comm.rank = rank;
   return SGLM_OK;
 }
@@ -2083,6 +2125,21 @@ int sglm_predict_new(sglm_engine* h, const double* X, int64_t n, int64_t p, int6
   return e->predict_new(X, n, p, ldx, beta, offset, m, family, link, type, out);
 }
 
+int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int family, int link, char* name,
+                         int64_t namelen) {
+  if (n < 1 || p < 1 || fused_split < 0 || !family_link_valid(family, link)) {
+    set_error("requirement failed: n >= 1, p >= 1, fused_split >= 0, a supported family/link");
+    return -1;
+  }
+  const int64_t n_pad = (n + RB - 1) / RB * RB;  // alloc_data's leading dimension
+  const bool proc = (flags & 1) != 0, wide = proc || (flags & 2) || p > 16 * MAX_P16, narrow = !wide && p <= 64;
+  const int P16 = wide ? 0 : narrow ? narrow_variant((int)p) : pass_variant((int)p);
+  char buf[64];
+  const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, family, link, buf, sizeof buf);
+  if (name && namelen > 0) std::snprintf(name, (size_t)namelen, "%s", buf);
+  return k;
+}
+
 int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   if (int rc = check_handle(h)) return rc;
   if (h->group()) {  // kernel times: the slowest shard; rows and bytes: all shards
@@ -2111,7 +2168,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
     out->comm_path = h->gcomms.empty() ? SGLM_COMM_GROUP_HOST : SGLM_COMM_GROUP_RCCL;
     out->rank_blocks = 1;
     out->solve_path = h->solve_path;
-    return SGLM_OK;
+    return SGLM_OK;  // pass_kernel / pass_kernel_name: shard 0's (every shard runs the same variant)
   }
   out->passes = h->passes;
   out->pass_kernel_ms = h->pass_ms;
@@ -2141,6 +2198,8 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->proc_chunks = h->nch;
   out->proc_chunk_rows = h->ch_rows;
   out->solve_path = h->solve_path;
+  out->pass_kernel = h->last_kernel;
+  std::memcpy(out->pass_kernel_name, h->last_kernel_name, sizeof out->pass_kernel_name);
   return SGLM_OK;
 }
 

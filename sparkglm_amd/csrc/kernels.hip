@@ -52,7 +52,10 @@ struct Geo {
   static constexpr int NA = NW - NRW;
   static constexpr int NI = NA > 0 ? NA : 1;
   static constexpr int QMAX = (4 * P16 + NI - 1) / NI;  // quads per issuer (at most)
-  static constexpr int VMAX = NI >= 4 ? 1 : 4 / NI;     // vectors per issuer (at most)
+  // vectors per issuer (at most), rounded UP so the NI issuers cover all four vectors (y, m,
+  // offset, prior): at P16 = 10 (NI = 3) 4 / NI dropped the prior weights (tests/test_gpu_fused_split.py)
+  static constexpr int VMAX = (4 + NI - 1) / NI;
+  static_assert(VMAX * NI >= 4, "every vector staged");
   // 16-column blocks of the image are BSTR = 16*RB + 2 doubles apart: the pad keeps the
   // compiler from pairing the per-block B-operand reads into ds_read2st64_b64 (32-bank rule,
   // 2-way conflicts under the slot swizzle, 8 LDS cycles) -- they stay ds_read_b64

@@ -150,23 +150,27 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 // carries them (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass, ~1 % at p = 64).
 // The Poisson / Gamma statistics' per-fit constants (rowmath.hpp init_stats_const) are summed by
 // the initial pass (IRLS = false) into S_AUX2.
-#ifndef SGLM_POIS_NOLOG
-#define SGLM_POIS_NOLOG 1  // Poisson IRLS rows: deviance without the per-row log (A/B builds: 0)
-#endif
 template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
-  // the initial pass of a Poisson fit: its per-row functions of the count y tabulated in LDS
-  // (rowmath.hpp poisson_init_table), after the waves' images
-  // (not at P16 = 2: its 32-row double-buffered images leave no 6 KB of the 160 KB)
-  constexpr bool PTAB = !IRLS && FAM == FAM_POISSON && (G::LDS + 3 * POIS_TAB + 8) * 8 <= 160 * 1024;
-  __shared__ double lds[G::LDS + (PTAB ? 3 * POIS_TAB + 8 : 0)];
+  // Poisson: per-row functions of the count y tabulated in LDS after the waves' images -- the
+  // initial pass's unit deviance at mu0 and lgamma(y + 1) (rowmath.hpp poisson_init_table), the
+  // IRLS passes' y log y (poisson_ylogy_table, pass_row ylogy)
+  constexpr bool PTAB = !IRLS && FAM == FAM_POISSON && (G::LDS + 2 * POIS_TAB + 8) * 8 <= 160 * 1024;
+  constexpr bool YTAB = IRLS && FAM == FAM_POISSON && (G::LDS + POIS_TAB) * 8 <= 160 * 1024;
+  static_assert(FAM != FAM_POISSON || PTAB || YTAB, "the Poisson tables fit every narrow variant's LDS");
+  __shared__ double lds[G::LDS + (PTAB ? 2 * POIS_TAB + 8 : (YTAB ? POIS_TAB : 0))];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double* wl = lds + wv * G::WAVE_LDS;
-  double* ptab = lds + G::LDS;     // [3][POIS_TAB] (PTAB)
-  double* pconst = ptab + 3 * POIS_TAB;  // init_const (PTAB)
+  double* ptab = lds + G::LDS;     // PTAB: [2][POIS_TAB]; YTAB: [POIS_TAB]
+  double* pconst = ptab + 2 * POIS_TAB;  // init_const (PTAB)
+  const double* ylogy = YTAB ? ptab : nullptr;
+  if constexpr (YTAB) {
+    for (int k = threadIdx.x; k < POIS_TAB; k += 64 * G::NW) poisson_ylogy_table(ptab, k);
+    __syncthreads();
+  }
   if constexpr (PTAB) {
     for (int k = threadIdx.x; k < POIS_TAB; k += 64 * G::NW) poisson_init_table(ptab, a.mu0, k);
     if (threadIdx.x == 0) {
@@ -293,14 +297,13 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         if (row < a.n) {
           const double y = hi ? y_p : yv, m = hi ? m_p : mv, off = hi ? off_p : ov, pw = hi ? pw_p : pv;
           if constexpr (STATS)
-            pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true);
-          else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
+            pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true, ylogy);
+          else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
-                     !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
+                     !IRLS, ylogy);
             if constexpr (INIT_CONST)
               if (mode != MODE_LM_GRAM) {
                 s_ll += init_stats_const<FAM>(y, pw);
-                if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
               }
           }
         }
@@ -381,15 +384,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if constexpr (STATS)
-          pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2);
-        else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll))) {
+          pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2, ylogy);
+        else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
-                   !IRLS, IRLS && FAM == FAM_POISSON && SGLM_POIS_NOLOG);
+                   !IRLS, ylogy);
           if constexpr (INIT_CONST)
-            if (mode != MODE_LM_GRAM) {
-              s_ll += init_stats_const<FAM>(y, pw);
-              if constexpr (FAM == FAM_POISSON) s_pear += poisson_dev_const_ref(y, pw);
-            }
+            if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
         }
       }
       wl[G::OFF_W + rl] = w;
@@ -501,7 +501,6 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       }
       if constexpr (INIT_CONST) {
         if (lane == S_AUX2) v = s_ll;
-        if (FAM == FAM_POISSON && lane == S_AUX1) v = s_pear;
       }
       out[G::T * 256 + G::NC + lane] = v;
     }

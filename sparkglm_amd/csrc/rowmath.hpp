@@ -160,6 +160,11 @@ struct RowAcc {
   double s[NS];
 };
 
+// Poisson counts y < POIS_TAB that are integers take their per-row functions of y from tables
+// built once per workgroup in LDS with the reference's own expressions (poisson_init_table,
+// poisson_ylogy_table below).
+constexpr int POIS_TAB = 256;
+
 // Unit deviance row value: devBinomial (GLM.scala:166-167) and the R families; the
 // family factor (2 for binomial / poisson / gamma) is applied on the host after summing.
 __device__ __forceinline__ double unit_dev(int fam, double y, double mu, double m, double pw) {
@@ -246,15 +251,17 @@ __device__ __forceinline__ void pass_row_init(const double* c, double y, double 
 // small_exp selects exp_small over libm's exp:
 // measured faster in the p <= 32 narrow pass (-1 %), slower at p = 64 (+4 %) and neutral in
 // the fused / wide kernels, so only the p <= 32 narrow variants set it.
-// dev_nolog (the narrow kernel's Poisson IRLS passes): the Poisson unit deviance without its
-// fit-constant part pw y log y (summed once by the initial pass into S_AUX1, poisson_dev_const;
-// the engine adds it back): pw (-y eta - (y - mu)) per row, no log -- the family arithmetic runs on
-// 16 of 64 lanes at p = 64, and log_pos was ~2/5 of it.
-__device__ __noinline__ double poisson_dev_const_ref(double y, double pw) { return y > 0.0 ? pw * (y * log(y)) : 0.0; }
+// ylogy (the narrow kernel's Poisson IRLS passes): an LDS table of k log k for the integer counts
+// k < POIS_TAB (poisson_ylogy_table), so that those rows need no log: the Poisson unit deviance
+// y log(y / mu) - (y - mu) = (y log y - y eta) - (y - mu) with y log y looked up.  The deviance stays
+// a per-row sum of terms of the size of the row's own deviance -- what GLM.scala:452's absolute tol
+// on the change needs (a round-3 form summed -y eta - (y - mu) per row and added sum y log y once
+// per pass: with counts ~1e3 over 1e8 rows its terms reached ~1e12 in total and their rounding,
+// ~1e-4, swamped tol 1e-6).  Other rows (non-integer or large y) take log_pos.
 __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta, double y, double m, double off,
                                          double pw, double mu0, double ybar, bool has_m, double& w, double& wz,
                                          double& s_dev, double& s_aux, bool small_exp = false,
-                                         bool init_fast = false, bool dev_nolog = false) {
+                                         bool init_fast = false, const double* ylogy = nullptr) {
   (void)ybar;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT && mode == MODE_IRLS && !has_m && fabs(eta) < 8.0 && y >= 0.0 &&
       y <= 1.0) {
@@ -280,15 +287,15 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
     // Poisson / log (R's poisson()): mu = exp(eta), g' = 1/mu, V = mu, so
     //   w = 1/(V g'^2) = mu,  w*z = mu (eta - off) + (y - mu),
     //   dev row = y log(y/mu) - (y - mu) with log(y/mu) = log(y) - eta
-    // -- one exp and one log, no divisions; the reference operation order (below) agrees to
-    // a few ulp per row, and it still runs where exp could overflow.
+    // -- one exp and one log (or a table look-up), no divisions; the reference operation order
+    // (below) agrees to a few ulp per row, and it still runs where exp could overflow.
     const double mu = small_exp ? exp_small(eta) : exp(eta);
     w = pw * mu;
     wz = pw * (mu * (eta - off) + (y - mu));
-    if (dev_nolog)
-      s_dev += pw * (-(y * eta) - (y - mu));
-    else
-      s_dev += pw * ((y > 0.0 ? y * (log_pos(y) - eta) : 0.0) - (y - mu));
+    double d0;
+    if (ylogy && y < (double)POIS_TAB && y == floor(y)) d0 = ylogy[(int)y] - y * eta;
+    else d0 = y > 0.0 ? y * (log_pos(y) - eta) : 0.0;
+    s_dev += pw * (d0 - (y - mu));
     s_aux += pw;
     return;
   }
@@ -325,7 +332,7 @@ __device__ __forceinline__ void pass_row(int fam, int lnk, int mode, double eta,
   const RowWZ r = pass_row_ref(fam, lnk, mode, eta, y, m, off, pw, mu0);
   w = r.w;
   wz = r.wz;
-  s_dev += (dev_nolog && fam == FAM_POISSON && mode == MODE_IRLS) ? r.dev - poisson_dev_const_ref(y, pw) : r.dev;
+  s_dev += r.dev;
   s_aux += pw;
 }
 
@@ -434,7 +441,6 @@ __device__ __noinline__ RowStats stats_row_fallback(int fam, int lnk, double eta
   } else if (fam == FAM_POISSON) {
     o.s3 = a.s[S_LL] + pw * lgamma(y + 1.0);  // the constant part is subtracted once per fit
     o.s4 = 0.0;
-    o.dev -= y > 0.0 ? pw * (y * log(y)) : 0.0;  // the deviance's constant part too (dev_nolog)
   } else {
     o.s3 = a.s[S_AUX0];
     o.s4 = a.s[S_LL] - a.s[S_AUX1];  // pw log y - pw log mu = pw log(y / mu)
@@ -477,12 +483,15 @@ __device__ __forceinline__ void pass_row_logit_stats(double eta, double y, doubl
 // Slots: s2 = Pearson, s3 = loglik part, s4 unused.
 __device__ __forceinline__ void pass_row_poisson_stats(double eta, double y, double off, double pw, double& w,
                                                        double& wz, double& s_dev, double& s_aux, double& s2,
-                                                       double& s3, bool small_exp) {
+                                                       double& s3, bool small_exp, const double* ylogy) {
   if (fabs(eta) < 700.0 && y >= 0.0 && y < 1e300) {
     const double mu = small_exp ? exp_small(eta) : exp(eta);
     w = pw * mu;
     wz = pw * (mu * (eta - off) + (y - mu));
-    s_dev += pw * (-(y * eta) - (y - mu));  // + pw y log y, summed by the initial pass (pass_row dev_nolog)
+    double d0;  // pass_row's Poisson unit deviance
+    if (ylogy && y < (double)POIS_TAB && y == floor(y)) d0 = ylogy[(int)y] - y * eta;
+    else d0 = y > 0.0 ? y * (log_pos(y) - eta) : 0.0;
+    s_dev += pw * (d0 - (y - mu));
     s_aux += pw;
     const double r = y - mu;
     s2 += pw * (r * r) * rcp_pos(mu);
@@ -492,7 +501,7 @@ __device__ __forceinline__ void pass_row_poisson_stats(double eta, double y, dou
   const RowStats r = stats_row_fallback(FAM_POISSON, LNK_LOG, eta, y, off, pw);
   w = r.w;
   wz = r.wz;
-  s_dev += r.dev;  // stats_row_fallback takes the y log y constant out (dev_nolog)
+  s_dev += r.dev;
   s_aux += pw;
   s2 += r.s2;
   s3 += r.s3;
@@ -532,8 +541,7 @@ __device__ __forceinline__ void pass_row_gamma_stats(double eta, double y, doubl
 }
 
 // The per-fit constants of the in-pass statistics, summed by the initial pass into S_AUX2:
-// Poisson sum pw lgamma(y + 1) (R's dpois), Gamma sum pw log y (R's dgamma).  Poisson also sums
-// its deviance constant pw y log y into S_AUX1 (poisson_dev_const_ref, pass_row dev_nolog).
+// Poisson sum pw lgamma(y + 1) (R's dpois), Gamma sum pw log y (R's dgamma).
 __device__ __noinline__ double init_stats_const_ref(int fam, double y, double pw) {
   return fam == FAM_POISSON ? pw * lgamma(y + 1.0) : pw * log(y);
 }
@@ -545,25 +553,26 @@ __device__ __forceinline__ double init_stats_const(double y, double pw) {
 
 // The initial pass of a Poisson fit (mu = mu0 for every row, GLM.scala:263-272, 429-444, R's
 // poisson()): per row, pass_row_ref needs log(y / mu0) for the unit deviance, and the in-pass
-// statistics' constants need lgamma(y + 1) and y log y (init_stats_const, poisson_dev_const_ref)
-// -- three libm calls on the 16 of 64 lanes of a p = 64 narrow pass.  Counts y are small
-// integers, so the three functions of k = y are tabulated once per workgroup for k < POIS_TAB
-// with the very same expressions (tab[k] = (k > 0 ? k log(k / mu0) : 0) - (k - mu0),
-// tab[T + k] = lgamma(k + 1), tab[2T + k] = (k > 0 ? k log k : 0)); a row then multiplies by
-// its prior weight exactly where the reference expressions do, so the rows are bitwise
-// pass_row_ref's.  Other rows (non-integer or large y) take the reference path.
-constexpr int POIS_TAB = 256;
+// statistics' constant needs lgamma(y + 1) (init_stats_const) -- two libm calls on the 16 of 64
+// lanes of a p = 64 narrow pass.  Counts y are small integers, so the two functions of k = y are
+// tabulated once per workgroup for k < POIS_TAB with the very same expressions
+// (tab[k] = (k > 0 ? k log(k / mu0) : 0) - (k - mu0), tab[T + k] = lgamma(k + 1)); a row then
+// multiplies by its prior weight exactly where the reference expressions do, so the rows are
+// bitwise pass_row_ref's.  Other rows (non-integer or large y) take the reference path.
 __device__ __forceinline__ void poisson_init_table(double* tab, double mu0, int k) {
   const double y = (double)k;
   tab[k] = (y > 0.0 ? y * log(y / mu0) : 0.0) - (y - mu0);
   tab[POIS_TAB + k] = lgamma(y + 1.0);
-  tab[2 * POIS_TAB + k] = y > 0.0 ? y * log(y) : 0.0;
 }
-// w, w*z from the init constants c (init_const), the deviance and the two statistics constants
-// from the table; false: the row is not a tabulated count (caller takes the reference path)
+// The IRLS passes' table (pass_row ylogy): k log k, 0 at k = 0.
+__device__ __forceinline__ void poisson_ylogy_table(double* tab, int k) {
+  const double y = (double)k;
+  tab[k] = y > 0.0 ? y * log(y) : 0.0;
+}
+// w, w*z from the init constants c (init_const), the deviance and the statistics constant from
+// the table; false: the row is not a tabulated count (caller takes the reference path)
 __device__ __forceinline__ bool poisson_init_row(const double* c, const double* tab, double y, double off, double pw,
-                                                 double& w, double& wz, double& s_dev, double& s_aux, double& s_dc,
-                                                 double& s_lg) {
+                                                 double& w, double& wz, double& s_dev, double& s_aux, double& s_lg) {
   if (!(y >= 0.0 && y < (double)POIS_TAB && y == floor(y))) return false;
   const int k = (int)y;
   w = pw * c[3];
@@ -572,7 +581,6 @@ __device__ __forceinline__ bool poisson_init_row(const double* c, const double* 
   s_dev += pw * tab[k];
   s_aux += pw;
   s_lg += pw * tab[POIS_TAB + k];
-  s_dc += k > 0 ? pw * tab[2 * POIS_TAB + k] : 0.0;
   return true;
 }
 
@@ -581,11 +589,11 @@ __device__ __forceinline__ bool poisson_init_row(const double* c, const double* 
 template <int FAM>
 __device__ __forceinline__ void pass_row_stats(double eta, double y, double off, double pw, double& w, double& wz,
                                                double& s_dev, double& s_aux, double& s2, double& s3, double& s4,
-                                               bool small_exp) {
+                                               bool small_exp, const double* ylogy = nullptr) {
   if constexpr (FAM == FAM_BINOMIAL)
     pass_row_logit_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, s4, small_exp);
   else if constexpr (FAM == FAM_POISSON)
-    pass_row_poisson_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, small_exp);
+    pass_row_poisson_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, small_exp, ylogy);
   else
     pass_row_gamma_stats(eta, y, off, pw, w, wz, s_dev, s_aux, s2, s3, s4);
 }

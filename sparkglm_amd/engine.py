@@ -298,6 +298,8 @@ class Engine:
         d = {k: getattr(s, k) for k, _ in L.Stats._fields_}
         d["comm_path_name"] = L.COMM_PATHS.get(d["comm_path"], "?")
         d["solve_path_name"] = L.SOLVE_PATHS.get(d["solve_path"], "?")
+        d["pass_kernel_name"] = s.pass_kernel_name.decode()
+        d["pass_kernel_kind"] = L.PASS_KERNELS.get(d["pass_kernel"], "?")
         return d
 
     def reset_stats(self):

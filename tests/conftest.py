@@ -58,3 +58,16 @@ def nrel(a, b):
     """Norm-wise relative difference max|a-b| / max|b| (for sums with cancellation)."""
     a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+
+# Per-coefficient bar for ill-conditioned solves (gamma designs): the solve's backward-error scale
+# cond * eps * max|b| / |b_i| times K = 20, the spread the reference's own algorithm shows between two
+# correct implementations of it on configs[3]'s X'WX (tests/golden/gram_split_p2048.json: LAPACK
+# dgetrf + dgetri against the oracle's unblocked restatement reaches K = 17.6).
+K_BOUND = 20.0
+
+
+def cond_ok(b, r, cond, tol=1e-9, k=K_BOUND):
+    b, r = np.asarray(b, dtype=np.float64), np.asarray(r, dtype=np.float64)
+    bound = np.maximum(tol, k * cond * np.finfo(float).eps * np.max(np.abs(r)) / np.abs(r))
+    return bool(np.all(np.abs(b - r) / np.abs(r) <= bound))

@@ -61,25 +61,29 @@ def test_config2_poisson_offset_prior_p64(eng):
     assert rel(f.dev_trace, o.dev_trace) < TOL
 
 
-# configs[3]'s conditioning floor (oracle/lu_floor.py, tests/golden/lu_floor_p2048.json): on the
-# oracle's OWN X'WX of the last solve (cond 3.3e5 at 6000 rows), LAPACK's dgetrf + dgetri -- Breeze
-# inv's algorithm as netlib-java binds it natively -- lands up to 1.6e-9 from the oracle's unblocked
-# restatement of the same algorithm, the product inv * X'Wz summed in another order 2.0e-9, and X'WX
-# re-summed in another order (2.4e-16 norm-wise) 2.8e-9: the smallest coefficients (|b| ~ 0.02
-# beside max ~ 50) are defined by the reference itself only to ~cond * eps * max|b|.  Bar: 1e-9
-# norm-wise for the coefficients, every other output elementwise at 1e-9, and each coefficient
-# elementwise at max(1e-9, 50 cond eps max|b| / |b_i|) with cond(X'WX) measured on the engine's own
-# Gram at the fit (the backward-error bound of a solve, per component; at 12.5M rows cond ~1e5 and
-# the smallest |b_i| ~1e-3 of max|b| give ~1e-7 on that one coefficient).
+# configs[3]'s conditioning floor.  On the full 12.5M x 2048 shard (oracle/gram_split.py,
+# tests/golden/gram_split_p2048.json, and test_config3_gram_and_solve_split below), at one beta:
+# the engine's X'WX equals the streaming oracle's to 7.5e-15 entrywise (1.2e-15 norm-wise), yet the
+# smallest coefficients (|b| ~ 0.009 beside max ~ 53; cond(X'WX) 9.8e4) move by ~3e-8 under ANY
+# ulp-level change of the solve: Breeze inv's own algorithm as LAPACK runs it (dgetrf + dgetri,
+# what netlib-java binds natively) against the oracle's unblocked restatement of it: 2.7e-8; the
+# engine's Cholesky against that LU on the same Gram: 2.7e-8; the oracle's LU on the engine's Gram
+# against it on the oracle's: 3.9e-8.  In units of the solve's backward-error scale per coefficient,
+# cond * eps * max|b| / |b_i|, the reference's own LAPACK-vs-restatement spread reaches K = 17.6 and
+# the engine's whole fit K = 5.9.  Bar: coefficients 1e-9 norm-wise, each within K_BOUND = 20 of
+# those units (the measured reference spread), every other output elementwise at 1e-9.
+K_BOUND = 20.0
+
+
 def wide_elementwise_ok(eng, f, ref, family, link):
     G, _, _ = eng.irls_pass(f.coefs, family=family, link=link)
     cond = float(np.linalg.cond(G))
     b, r = np.asarray(f.coefs), np.asarray(ref)
-    bound = np.maximum(TOL, 50 * cond * np.finfo(float).eps * np.max(np.abs(r)) / np.abs(r))
+    bound = np.maximum(TOL, K_BOUND * cond * np.finfo(float).eps * np.max(np.abs(r)) / np.abs(r))
     err = np.abs(b - r) / np.abs(r)
     i = int(np.argmax(err / bound))
     print(f"coefs elementwise {err.max():.2e}; worst vs its bound: |b| {abs(r[i]):.2e} err {err[i]:.2e} "
-          f"bound {bound[i]:.2e} (cond {cond:.1e})")
+          f"bound {bound[i]:.2e} (cond {cond:.1e}; K = {err[i] / bound[i] * K_BOUND:.2f})")
     return bool(np.all(err <= bound))
 
 
@@ -98,6 +102,51 @@ def test_config3_gamma_p2048(eng):
     assert wide_elementwise_ok(eng, f, o.coefs, "gamma", "inverse")
     assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
                [o.deviance, o.null_deviance, o.pearson, o.loglik]) < TOL
+
+
+GRAM_SPLIT = os.path.join(GOLDEN, "gram_split_p2048.npz")
+
+
+@pytest.mark.skipif(not os.path.exists(GRAM_SPLIT) or not os.path.exists(os.path.join(GOLDEN, "full_scale.json")),
+                    reason="gram_split fixture absent")
+def test_config3_gram_and_solve_split(eng):
+    """Where configs[3]'s elementwise coefficient error comes from, on the full 12.5M x 2048 gamma
+    shard at the oracle's final coefficients (oracle/gram_split.py): (a) the engine's X'WX / X'Wz
+    against the streaming oracle's -- a digest of it: diag, X'WX V for 8 fixed probe vectors, X'Wz;
+    (b) the engine's own solve (rocSOLVER Cholesky) against the oracle's LU inverse (Breeze inv,
+    utils.scala:103-105, 134-136) applied to the ENGINE's Gram; (c) that LU on the engine's Gram
+    against it on the oracle's.  (b) and (c) are the two sources; each stays inside K_BOUND of the
+    solve's backward-error units, the spread the reference's own LAPACK LU shows on this matrix."""
+    z = np.load(GRAM_SPLIT)
+    c = _full_scale()["gamma2048"]
+    beta = z["beta"]
+    eng.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"])
+    G, xtwz, s = eng.irls_pass(beta, family="gamma", link="inverse")
+    x_chol, _ = eng.irls_iterations(beta, 1, "gamma", "inverse")
+    assert eng.stats()["solve_path_name"] == "device-cholesky"
+    eng.synth(c["kind"], 0, 64, c["p"], c["seed"])  # release the full-size shard
+    p = G.shape[0]
+    # (a) the Gram: entrywise on the diagonal, norm-wise on the probe products, X'Wz, deviance
+    V = np.random.default_rng(20481).uniform(-1.0, 1.0, size=(p, 8))
+    d_diag = rel(np.diag(G), z["diag"])
+    d_gv = float(np.linalg.norm(G @ V - z["GV"]) / np.linalg.norm(z["GV"]))
+    d_xz = rel(xtwz, z["xtwz"])
+    print(f"\n(a) diag {d_diag:.2e}  X'WX V norm-wise {d_gv:.2e}  X'Wz {d_xz:.2e}  deviance {rel(s[0], z['s'][0]):.2e}")
+    assert d_diag < 1e-13 and d_gv < 1e-14 and d_xz < 1e-13 and rel(s[0], z["s"][0]) < 1e-13
+    # (b) / (c): the oracle's LU (dgetrf + dgetri, inv * b in order) on the engine's Gram
+    Gi = po.lu_inverse(G)
+    x_lu = np.zeros(p)
+    for k in range(p):
+        x_lu = x_lu + Gi[:, k] * xtwz[k]
+    x_ref = z["x_lu_oracle"]
+    unit = np.linalg.cond(G) * np.finfo(float).eps * np.max(np.abs(x_ref)) / np.abs(x_ref)
+    kb = float(np.max(np.abs(x_chol - x_lu) / np.abs(x_lu) / unit))
+    kc = float(np.max(np.abs(x_lu - x_ref) / np.abs(x_ref) / unit))
+    kt = float(np.max(np.abs(x_chol - x_ref) / np.abs(x_ref) / unit))
+    print(f"(b) Cholesky vs LU on the engine's Gram: {rel(x_chol, x_lu):.2e} (K {kb:.1f}); (c) LU on the engine's vs "
+          f"the oracle's Gram: {rel(x_lu, x_ref):.2e} (K {kc:.1f}); total {rel(x_chol, x_ref):.2e} (K {kt:.1f})")
+    assert nrel(x_chol, x_ref) < 1e-9 and nrel(x_lu, x_ref) < 1e-9
+    assert kb < K_BOUND and kc < K_BOUND and kt < K_BOUND
 
 
 def _full_scale():

@@ -1,12 +1,18 @@
-"""The split-role fused pass K1r (kernels.hip irls_pass_r_kernel, 225 <= p <= 256: two MFMA-only
-"Gram waves" and one "row wave" per SIMD) against K1 (irls_pass_kernel<16>, SGLM_FUSED_SPLIT=0,
-read when an engine is created).  K1r accumulates every Gram tile and X'Wz column in K1's order
-(same k-steps, blocks and lanes) and its row stage is K1's, so one pass and a whole fit must come
-out BITWISE the same -- for every family / link and with offset + prior weights (the row stage's
-four vectors, staged by the four row waves), at p = 256 and at p = 232 (column quads past p are
+"""The split-role fused pass K1r (kernels.hip irls_pass_r_kernel: two MFMA-only "Gram waves" and
+one "row wave" per SIMD) against K1 (irls_pass_kernel, SGLM_FUSED_SPLIT=0, read when an engine is
+created).
+
+At P16 = 16 (225 <= p <= 256) K1r accumulates every Gram tile and X'Wz column in K1's order (same
+k-steps, blocks and lanes) and its row stage is K1's, so one pass and a whole fit must come out
+BITWISE the same -- for every family / link and with offset + prior weights (the row stage's four
+vectors, staged by the four row waves), at p = 256 and at p = 232 (column quads past p are
 duplicated into the padded LDS image), over shards that split into ragged row ranges per
-workgroup, and for a shard smaller than one row block per workgroup.  Both sides are also held
-to the oracle (partitionComponents / zwCreateBinomial, GLM.scala:359-395, utils.scala:84-92)."""
+workgroup, and for a shard smaller than one row block per workgroup.
+
+Below P16 = 16 (the mid-width generalisation, K1r by default from P16 = 10) the Gram waves own other
+tile runs than K1's waves and the row stage reads another lane layout: NOT bitwise.  There both
+kernels are held to the oracle (partitionComponents / zwCreateBinomial, GLM.scala:359-395,
+utils.scala:84-92) at 1e-9 with the same iteration count, and to each other at 1e-12."""
 import os
 
 import numpy as np
@@ -64,6 +70,70 @@ def test_pass_and_fit_bitwise_k1(label, kind, n, p, family, link):
     assert np.array_equal(np.asarray(f0.stderr), np.asarray(f1.stderr))
     assert (f0.deviance, f0.null_deviance, f0.pearson, f0.loglik) == (f1.deviance, f1.null_deviance, f1.pearson,
                                                                       f1.loglik)
+
+
+MID = [
+    # (label, synth kind, rows, p, family, link, K1r threshold SGLM_FUSED_SPLIT)
+    ("p150 poisson + offset + prior", 2, 120_001, 150, "poisson", "log", "1"),
+    ("p200 gamma", 3, 60_000, 200, "gamma", "inverse", "1"),
+    ("p180 logit, fewer blocks than workgroups", 0, 3_000, 180, "binomial", "logit", "1"),
+    ("p129 probit", 0, 90_000, 129, "binomial", "probit", "1"),
+    ("p96 cloglog, K1r forced from P16 = 6", 0, 100_000, 96, "binomial", "cloglog", "6"),
+    ("p112 poisson + offset + prior, K1r forced from P16 = 6", 2, 80_000, 112, "poisson", "log", "6"),
+]
+
+
+@pytest.mark.parametrize("label,kind,n,p,family,link,thr", MID, ids=[c[0] for c in MID])
+def test_mid_width_k1r_and_k1_match_oracle(label, kind, n, p, family, link, thr):
+    import pyoracle  # checker only
+    from conftest import cond_ok, nrel, rel
+    fits = {}
+    for split, env in (("K1", "0"), ("K1r", thr)):
+        saved = os.environ.get("SGLM_FUSED_SPLIT")
+        os.environ["SGLM_FUSED_SPLIT"] = env
+        try:
+            e = Engine(0)
+        finally:
+            if saved is None:
+                os.environ.pop("SGLM_FUSED_SPLIT", None)
+            else:
+                os.environ["SGLM_FUSED_SPLIT"] = saved
+        with e:
+            e.synth(kind, 0, n, p, 13)
+            f = e.fit_glm(family, link)
+            kk = e.stats()["pass_kernel_kind"]
+            if split == "K1r":
+                X, y, m, off, pr = e.get_data()
+                cond = float(np.linalg.cond(e.irls_pass(f.coefs, family=family, link=link)[0]))
+        assert kk == ("fused" if split == "K1" else "fused-split"), (split, kk)
+        fits[split] = f
+    kw = dict(offset=off, prior=pr) if kind == 2 else {}
+    o = pyoracle.fit_glm(X, y, family, link, nthreads=8, **kw)
+    for split, f in fits.items():
+        assert f.iter == o.iter, (label, split)
+        # coefficients: 1e-9 elementwise, or -- gamma's ill-conditioned positive designs -- 1e-9
+        # norm-wise and each within the solve's backward-error bound (conftest.cond_ok)
+        if family == "gamma":
+            assert nrel(f.coefs, o.coefs) < 1e-9 and cond_ok(f.coefs, o.coefs, cond), (label, split, cond)
+        else:
+            assert rel(f.coefs, o.coefs) < 1e-9, (label, split)
+        assert rel(f.stderr, o.stderr) < 1e-9, (label, split)
+        assert rel([f.deviance, f.null_deviance, f.pearson, f.loglik],
+                   [o.deviance, o.null_deviance, o.pearson, o.loglik]) < 1e-9, (label, split)
+        assert rel(f.dev_trace, o.dev_trace) < 1e-9
+    a, b = fits["K1"], fits["K1r"]  # the two kernels' Grams differ by summation order only
+    assert (nrel if family == "gamma" else rel)(a.coefs, b.coefs) < 1e-10
+    assert rel(a.stderr, b.stderr) < 1e-10 and rel(a.deviance, b.deviance) < 1e-12
+
+
+def test_p160_shard_reports_k1r():
+    """The bench / roofline label comes from the engine's dispatch (sglm_stats.pass_kernel_name)."""
+    with Engine(0) as e:
+        e.synth(0, 0, 50_000, 160, 3)
+        e.irls_pass(np.full(160, 0.01))
+        st = e.stats()
+    assert st["pass_kernel_kind"] == "fused-split"
+    assert st["pass_kernel_name"] == "irls_pass_r_kernel<10,binomial,logit>"
 
 
 def test_split_pass_matches_oracle():

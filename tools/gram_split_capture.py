@@ -30,11 +30,18 @@ def main():
         G, xtwz, s = e.irls_pass(beta, family=c["family"], link=c["link"])
         x_chol, dev = e.irls_iterations(beta, 1, c["family"], c["link"])  # pass at beta + the device solve
         st = e.stats()
+    # the engine's LU route (SGLM_WIDE_SOLVE=lu: rocSOLVER getrf + getri, coefs = inv * X'Wz in order)
+    os.environ["SGLM_WIDE_SOLVE"] = "lu"
+    with Engine(0) as e:
+        e.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"])
+        x_lu_roc, _ = e.irls_iterations(beta, 1, c["family"], c["link"])
+        assert e.stats()["solve_path_name"] == "device-lu"
+    del os.environ["SGLM_WIDE_SOLVE"]
     p = G.shape[0]
     i, j = np.tril_indices(p)
     packed = np.empty(p * (p + 1) // 2)
     packed[i * (i + 1) // 2 + j] = G[i, j]
-    np.savez(os.path.join(out, "engine.npz"), beta=beta, G=packed, xtwz=xtwz, s=s, x_chol=x_chol,
+    np.savez(os.path.join(out, "engine.npz"), beta=beta, G=packed, xtwz=xtwz, s=s, x_chol=x_chol, x_lu_roc=x_lu_roc,
              fit_coefs=f.coefs, fit_iter=f.iter, solve_path=st["solve_path_name"])
     print(f"solve path {st['solve_path_name']}; saved in {time.time() - t0:.1f} s", flush=True)
 

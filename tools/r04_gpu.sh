@@ -9,10 +9,26 @@ if [[ ,$STAGES, == *,cap,* ]]; then
   tail -3 gpurun_out/cap.log
 fi
 if [[ ,$STAGES, == *,test,* ]]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -W ignore > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -rA --timeout 300 --timeout-method thread -W ignore > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
   timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
   cat gpurun_out/smoke.log
+fi
+if [[ ,$STAGES, == *,ab,* ]]; then  # same-box A/B: the round-3 library (lib_ab/head) against the tree
+  export AB_LIBS=sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so AB_REPS=3
+  AN=200000000 AP=32 AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p32.log 2>&1 || { echo "ab p32 failed"; tail gpurun_out/ab_p32.log; exit 1; }
+  AN=125000000 AP=64 AK=2 AF=poisson AL=log timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p64.log 2>&1 || { echo "ab p64 failed"; tail gpurun_out/ab_p64.log; exit 1; }
+  cat gpurun_out/ab_p32.log gpurun_out/ab_p64.log
+fi
+if [[ ,$STAGES, == *,benchw,* ]]; then  # the other workloads' bench lines (WORKLOADS env: space-separated)
+  for w in ${WORKLOADS:-poisson64}; do
+    timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-load > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { echo "bench $w failed"; tail -20 gpurun_out/bench_$w.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/bench_$w.json')); r=d['roofline']; print('$w', d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], d['iters_to_converge'])"
+  done
+fi
+if [[ ,$STAGES, == *,rehearse8,* ]]; then  # 8 ranks sharing this GPU over gloo (the 8-GPU launch path)
+  timeout -k 10 900 python bench.py --gpus 8 --rows 10000000 --steps 3 --warmup 1 --no-load > gpurun_out/bench_gpus8.json 2> gpurun_out/bench_gpus8.err || { echo "rehearsal failed"; tail -20 gpurun_out/bench_gpus8.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_gpus8.json')); s=d['strong_scaling_1b_logit']; print('gpus8', d['n_gpus'], d['ms_per_step'], d['iters_to_converge'], s['n_gpus'], s['iters_to_converge'], repr(s['deviance']))"
 fi
 if [[ ,$STAGES, == *,bench,* ]]; then
   timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }

@@ -192,6 +192,8 @@ typedef struct {
   int pass_kernel;          /* enum sglm_pass_kernel of the last pass (the engine's own choice: the K1 / K1r
                                threshold, its row limit, the narrow / wide paths) */
   char pass_kernel_name[64];/* that kernel's name as rocprofv3 lists it, e.g. "irls_pass_r_kernel<16,binomial,logit>" */
+  int64_t lm_device_fits;   /* LM fits done in one device round trip (Gram pass, device Cholesky, residual pass;
+                               resident p <= 64 shards without a communicator; SGLM_LM_DEVICE=0 disables) */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device

@@ -135,6 +135,10 @@ struct StatsArgs {
   int family, link, mode;
   double mu0, ybar;
   double* partials;     // [grid][NS]
+  const double* ybar_dev;  // non-null: ybar read from the device (the LM device round trip, lm_chol_kernel)
+  int beta_by_value;    // p <= STATS_BETA_MAX: beta travels in the kernel arguments (no H2D copy)
+  double bv[32];        //   beta_by_value: beta[0..p)
 };
+constexpr int STATS_BETA_MAX = 32;
 
 }  // namespace sglm

@@ -219,8 +219,11 @@ int irls_iterate(Backend& be, const sglm_glm_opts& o, double* beta, int iters, d
 // LM.fit (LM.scala:241-274) over fitMultiple's components (LM.scala:217-237).
 int lm_drive(Backend& be, sglm_prelm* out) {
   const int64_t p = be.ncols();
-  std::vector<double> packed((size_t)packed_len(p)), s(NS);
-  int rc = be.pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, packed.data());
+  std::vector<double> packed((size_t)packed_len(p)), s(NS), dev_coefs((size_t)p);
+  bool dev = false;  // Gram pass, device solve and residual pass in one round trip (Backend::lm_device)
+  int rc = be.lm_device(packed.data(), dev_coefs.data(), s.data(), dev);
+  if (rc) return rc;
+  if (!dev) rc = be.pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, packed.data());
   if (rc) return rc;
   const double ysum = packed[tri_count(p) + p + S_DEV], nrow = packed[tri_count(p) + p + S_SUMW];
   std::unique_ptr<SolverIface> solver = be.make_solver(p);
@@ -237,8 +240,11 @@ int lm_drive(Backend& be, sglm_prelm* out) {
   be.solve_ms += now_ms() - t0;
   be.solve_path = solver->path();
   const double ymean = ysum / nrow;  // LM.scala:167-168
-  rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
-  if (rc) return rc;
+  // the device's residual statistics stand only if its solve was this one, bit for bit
+  if (!dev || std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
+    rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
+    if (rc) return rc;
+  }
   const double sse = s[S_DEV], top = s[S_PEARSON], bot = s[S_LL];
   const double r2 = top / bot;                                                      // LM.scala:185
   const double fstat = ((bot - sse) / ((double)p - 1.0)) / (sse / (nrow - (double)p));  // LM.scala:186

@@ -67,6 +67,20 @@ class Backend {
   virtual int pass_dev(int mode, const double* beta, double mu0, double ybar, int family, int link, double* packed) {
     return pass(mode, beta, mu0, ybar, family, link, packed);
   }
+  // LM.fit in one device round trip (lm_drive): the LM Gram pass, a device Cholesky solve in the
+  // host solver's exact operation order, and the residual pass at those coefficients, with one
+  // synchronisation.  Fills packed (the all-reduced Gram pass), dev_coefs and s (the residual
+  // statistics at dev_coefs) and sets done; done = false: not available here (lm_drive then takes
+  // the host round trips).  lm_drive keeps its host solve as the arbiter: when that solve does not
+  // reproduce dev_coefs bitwise (the LU fallback of an ill-conditioned X'X) it reruns the residual
+  // pass at its own coefficients.
+  virtual int lm_device(double* packed, double* dev_coefs, double* s, bool& done) {
+    (void)packed;
+    (void)dev_coefs;
+    (void)s;
+    done = false;
+    return SGLM_OK;
+  }
   // The solver for this backend's systems (default: host).
   virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats

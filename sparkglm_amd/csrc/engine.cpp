@@ -250,6 +250,8 @@ struct sglm_engine : public Backend {
   int64_t passes = 0, dev_passes = 0;
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
+  bool allow_lm_device = true;  // SGLM_LM_DEVICE=0: LM fits take the two host round trips (tests)
+  int64_t lm_device_fits = 0;
   int last_kernel = SGLM_KERNEL_NONE;  // the kernel of the last pass (enum sglm_pass_kernel) and its name
   char last_kernel_name[64] = "";
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
@@ -321,7 +323,7 @@ struct sglm_engine : public Backend {
     blas = nullptr;
     if (evm) (void)hipEventDestroy(evm);
     evm = nullptr;
-    for (double** ptr : {&hbeta, &hred}) {
+    for (double** ptr : {&hbeta, &hred, &hsmall}) {
       if (*ptr) (void)hipHostFree(*ptr);
       *ptr = nullptr;
     }
@@ -394,7 +396,9 @@ struct sglm_engine : public Backend {
   // known own rank; otherwise the communicator's plain sum
   bool gather_ranks() const { return comm.kind != 0 && comm.nranks > 1 && comm.rank >= 0 && comm.rank < comm.nranks; }
   int64_t dsmall_cap = 0;
+  double* hsmall = nullptr;  // pinned [64]: the final statistics' sums (stats)
   int ensure_small(int64_t count) {
+    if (!hsmall) HIPCHK(hipHostMalloc(&hsmall, sizeof(double) * 64, hipHostMallocDefault));
     if (count <= dsmall_cap && dsmall) return SGLM_OK;
     if (dsmall) HIPCHK(hipFree(dsmall));
     dsmall = nullptr;
@@ -1299,6 +1303,51 @@ struct sglm_engine : public Backend {
     return SGLM_OK;
   }
 
+  // LM.fit in one round trip (driver.hpp Backend::lm_device): a resident narrow shard with no
+  // communicator -- the Gram pass, lm_chol_kernel (the host Cholesky, bitwise, on the device), the
+  // residual pass at its coefficients (beta and ybar read from the device) and the device sum of its
+  // statistics, then ONE copy back and one synchronisation.  configs[0] (1M x 20) is launch- and
+  // latency-bound: this removes the host round trip between the two passes.
+  int lm_device(double* packed, double* dev_coefs, double* s, bool& done) override {
+    done = false;
+    if (!allow_lm_device || group() || comm.kind != 0 || wide || procx.on || !narrow || p > 64 || nblocks <= 0)
+      return SGLM_OK;
+    HIPCHK(hipSetDevice(device));
+    const int64_t plen = packed_len(p);
+    if (int rc = ensure_red_len(plen)) return rc;
+    if (int rc = ensure_small(64)) return rc;
+    if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY)) return rc;
+    double* aux = dsmall + NS;  // {ybar, leave-Cholesky flag}
+    HIPCHK(launch_lm_chol(dred, (int)p, LU_SWITCH_RATIO, dbeta, aux, st));
+    StatsArgs a{};
+    a.X = dX;
+    a.ld = n_pad;
+    a.p = (int)p;
+    a.beta = dbeta;
+    a.ybar_dev = aux;
+    a.y = dy;
+    a.n = n;
+    a.family = FAM_GAUSSIAN;
+    a.link = LNK_IDENTITY;
+    a.mode = MODE_LM_RESID;
+    a.partials = dpart;
+    const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
+    HIPCHK(launch_stats(a, nb, st));
+    HIPCHK(launch_reduce_stats(dpart, nb, dsmall, st));
+    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * plen, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hsmall, dsmall, sizeof(double) * NS, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hbeta, dbeta, sizeof(double) * p, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (int rc = pass_timing()) return rc;
+    red_on_device = true;
+    std::memcpy(packed, hred, sizeof(double) * plen);
+    std::memcpy(s, hsmall, sizeof(double) * NS);
+    std::memcpy(dev_coefs, hbeta, sizeof(double) * p);
+    done = true;
+    lm_device_fits += 1;
+    return SGLM_OK;
+  }
+
   std::unique_ptr<SolverIface> make_solver(int64_t pp) override;
   int blas_handle() {
     if (!blas) {
@@ -1324,17 +1373,22 @@ struct sglm_engine : public Backend {
       return SGLM_OK;
     }
     HIPCHK(hipSetDevice(device));
-    if (mode == MODE_LM_RESID) {  // pred = X * coefs into the eta buffer
+    StatsArgs a{};
+    // LM residuals of a narrow resident design: beta rides in the kernel arguments (no H2D copy on
+    // the fit's critical path, configs[0] is launch- and latency-bound)
+    const bool by_value = mode == MODE_LM_RESID && !procx.on && p <= STATS_BETA_MAX;
+    if (mode == MODE_LM_RESID && !by_value) {  // pred = X * coefs into the eta buffer
       std::memcpy(hbeta, beta, sizeof(double) * p);
       HIPCHK(hipMemcpyAsync(dbeta, hbeta, sizeof(double) * p, hipMemcpyHostToDevice, st));
       if (procx.on) HIPCHK(launch_predict(dX, n_pad, (int)p, n, dbeta, nullptr, deta, st, procx));
     }
-    StatsArgs a{};
     if (mode == MODE_LM_RESID && !procx.on) {  // one read of X, no eta round trip
       a.X = dX;
       a.ld = n_pad;
       a.p = (int)p;
       a.beta = dbeta;
+      a.beta_by_value = by_value ? 1 : 0;
+      if (by_value) std::memcpy(a.bv, beta, sizeof(double) * p);
     }
     a.y = dy;
     a.m = (mode == MODE_LM_RESID) ? nullptr : dm;
@@ -1348,17 +1402,15 @@ struct sglm_engine : public Backend {
     a.ybar = ybar;
     a.partials = dpart;
     // one wave per SIMD leaves the per-row chain latency-bound on large shards; small ones
-    // (LM 1M x 20) keep 1024 partials for the host-side sum
+    // (LM 1M x 20) keep 1024 partials; they are summed on the device (reduce_stats_kernel,
+    // compensated) and only the NS sums come back
     const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
     HIPCHK(launch_stats(a, nb, st));
-    std::vector<double> h((size_t)nb * NS);
-    HIPCHK(hipMemcpyAsync(h.data(), dpart, sizeof(double) * h.size(), hipMemcpyDeviceToHost, st));
+    if (int rc = ensure_small(64)) return rc;
+    HIPCHK(launch_reduce_stats(dpart, nb, dsmall, st));
+    HIPCHK(hipMemcpyAsync(hsmall, dsmall, sizeof(double) * NS, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    for (int k = 0; k < NS; ++k) {
-      double v = 0.0, c = 0.0;
-      for (int b = 0; b < nb; ++b) neumaier_add(v, c, h[(size_t)b * NS + k]);
-      s[k] = v + c;
-    }
+    std::memcpy(s, hsmall, sizeof(double) * NS);
     return allreduce_small(s, NS);
   }
 };
@@ -1672,6 +1724,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
+  if (const char* ld = std::getenv("SGLM_LM_DEVICE")) h->allow_lm_device = std::atoi(ld) != 0;
   if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::max(0, std::atoi(fs));
   if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "lu") == 0;
   if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
@@ -2199,6 +2252,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->proc_chunk_rows = h->ch_rows;
   out->solve_path = h->solve_path;
   out->pass_kernel = h->last_kernel;
+  out->lm_device_fits = h->lm_device_fits;
   std::memcpy(out->pass_kernel_name, h->last_kernel_name, sizeof out->pass_kernel_name);
   return SGLM_OK;
 }
@@ -2206,7 +2260,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
-  h->passes = h->dev_passes = 0;
+  h->passes = h->dev_passes = h->lm_device_fits = 0;
   h->pass_ms = h->reduce_ms = h->last_pass_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;

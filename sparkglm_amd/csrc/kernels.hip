@@ -72,7 +72,11 @@ struct Geo {
   static constexpr int LDS_DOUBLES = OFF_FLAG + 1;
   static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
   // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
-  static constexpr int WG_PER_CU = (8 / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? 8 / NW : 160 * 1024 / (LDS_DOUBLES * 8);
+#ifndef SGLM_EXP_WAVES
+#define SGLM_EXP_WAVES 8
+#endif
+  static constexpr int WMAX = SGLM_EXP_WAVES;  // EXPERIMENT (tools/ab.py): waves per CU wanted
+  static constexpr int WG_PER_CU = (WMAX / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? WMAX / NW : 160 * 1024 / (LDS_DOUBLES * 8);
   static constexpr int WAVES_PER_SIMD = (WG_PER_CU * NW + 3) / 4;
   // Block rows of wave wv's tiles: HI = P16-1-wv and LO below.  The row waves carry the row
   // stage on top of their MFMAs, so they take the LOW rows 0..NRW-1 (fewest tiles) and the
@@ -1019,16 +1023,20 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   for (int k = 0; k < NS; ++k) acc.s[k] = 0.0;
   const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = (lo + per < a.n) ? lo + per : a.n;
+  const double ybar = a.ybar_dev ? *a.ybar_dev : a.ybar;
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const double m = a.m ? a.m[i] : 1.0;
     const double pw = a.prior ? a.prior[i] : 1.0;
     double eta = 0.0;
     if (a.X) {  // LM residuals: X*coefs in predict_kernel's order (LM.scala:173-174)
-      for (int j = 0; j < a.p; ++j) eta += a.X[(int64_t)j * a.ld + i] * a.beta[j];
+      if (a.beta_by_value)
+        for (int j = 0; j < a.p; ++j) eta += a.X[(int64_t)j * a.ld + i] * a.bv[j];
+      else
+        for (int j = 0; j < a.p; ++j) eta += a.X[(int64_t)j * a.ld + i] * a.beta[j];
     } else if (a.eta) {
       eta = a.eta[i];
     }
-    stats_row(FAM, LNK, a.mode, eta, a.y[i], m, pw, a.mu0, a.ybar, a.m != nullptr, acc);
+    stats_row(FAM, LNK, a.mode, eta, a.y[i], m, pw, a.mu0, ybar, a.m != nullptr, acc);
   }
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -1040,6 +1048,103 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   if (threadIdx.x < NS) {
     const int k = threadIdx.x;
     a.partials[(int64_t)blockIdx.x * NS + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+  }
+}
+
+// LM.fit's p x p solve on the device (engine.cpp lm_device; p <= 64): the host solver's Cholesky
+// (solve.cpp chol_factor + chol_solve), element for element in the same operation order without
+// contraction, so the coefficients come out bitwise the host's (driver.cpp lm_drive checks that and
+// otherwise reruns the residual pass at its own).  Lane i owns row i: every column update is
+// lane-parallel with each element's subtractions in the host's k order; the back substitution's
+// dependent sums run on lane 0 in the host's order.  Out: beta[p]; aux[0] = sum y / rows (LM.scala:
+// 167-168), aux[1] = 1 where the host would leave Cholesky (a non-positive pivot, or the pivot
+// ratio below LU_SWITCH_RATIO: solve.cpp chol_pivot_ratio).
+__global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
+                                                     double* __restrict__ beta, double* __restrict__ aux) {
+#pragma clang fp contract(off)
+  __shared__ double A[64 * 64], dg[64], t[64];
+  const int i = threadIdx.x;
+  const int64_t tri = (int64_t)p * (p + 1) / 2;
+  for (int e = i; e < p * p; e += 64) {  // unpack_gram: A(r, c) = packed[max(r, c) (max + 1) / 2 + min(r, c)]
+    const int r = e % p, c = e / p, hi = r > c ? r : c, lo = r > c ? c : r;
+    A[e] = packed[hi * (hi + 1) / 2 + lo];
+  }
+  if (i < p) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
+  __syncthreads();
+  int fail = 0;
+  for (int j = 0; j < p; ++j) {  // chol_factor (left-looking jki)
+    double aj = (i < p) ? A[i + j * p] : 0.0;
+    for (int k = 0; k < j; ++k) {
+      const double ljk = A[j + k * p];
+      if (ljk == 0.0) continue;
+      if (i >= j && i < p) aj -= A[i + k * p] * ljk;
+    }
+    if (i >= j && i < p) A[i + j * p] = aj;
+    __syncthreads();
+    const double d = A[j + j * p];
+    if (!(d > 0.0) || !isfinite(d)) {
+      fail = 1;
+      break;
+    }
+    const double s = sqrt(d);
+    const double inv = 1.0 / s;
+    __syncthreads();
+    if (i == j) A[j + j * p] = s;
+    if (i > j && i < p) A[i + j * p] = aj * inv;
+    __syncthreads();
+  }
+  double ti = 0.0;
+  if (!fail) {
+    ti = (i < p) ? packed[tri + i] : 0.0;  // chol_solve: L t = b, column sweep
+    for (int j = 0; j < p; ++j) {
+      if (i == j) t[j] = ti / A[j + j * p];
+      __syncthreads();
+      const double tj = t[j];
+      if (i == j) ti = tj;
+      if (i > j && i < p) ti -= A[i + j * p] * tj;
+    }
+    if (i == 0) {  // L' x = t, dependent sums in the host's order
+      for (int r = p - 1; r >= 0; --r) {
+        double s = t[r];
+        for (int k = r + 1; k < p; ++k) s -= A[k + r * p] * t[k];
+        t[r] = s / A[r + r * p];
+      }
+    }
+    __syncthreads();
+    if (i < p) beta[i] = t[i];
+  }
+  if (i == 0) {
+    double r = 1.0;  // chol_pivot_ratio
+    if (!fail)
+      for (int j = 0; j < p; ++j) {
+        const double l = A[j + j * p], a = dg[j];
+        if (a > 0.0) r = fmin(r, (l * l) / a);
+      }
+    aux[0] = packed[tri + p + S_DEV] / packed[tri + p + S_SUMW];
+    aux[1] = (fail || r < ratio_min) ? 1.0 : 0.0;
+  }
+}
+
+// The stats partials [nparts][NS] summed on the device into out[NS] (no D2H of the partials):
+// thread (segment s, scalar k) sums partials [s n / 32, (s+1) n / 32) in order, Neumaier-compensated,
+// then thread k adds the 32 segment sums and their compensations in segment order.
+__global__ void __launch_bounds__(256) reduce_stats_kernel(const double* __restrict__ part, int nparts,
+                                                           double* __restrict__ out) {
+  __shared__ double ss[32][NS], cs[32][NS];
+  const int k = threadIdx.x % NS, sg = threadIdx.x / NS;
+  const int g0 = (int)((int64_t)nparts * sg / 32), g1 = (int)((int64_t)nparts * (sg + 1) / 32);
+  double s = 0.0, c = 0.0;
+  for (int g = g0; g < g1; ++g) neumaier_add(s, c, part[(int64_t)g * NS + k]);
+  ss[sg][k] = s;
+  cs[sg][k] = c;
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    double t = 0.0, tc = 0.0;
+    for (int q = 0; q < 32; ++q) {
+      neumaier_add(t, tc, ss[q][threadIdx.x]);
+      tc += cs[q][threadIdx.x];
+    }
+    out[threadIdx.x] = t + tc;
   }
 }
 
@@ -1174,6 +1279,17 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st) {
     case 16: return launch_pass_p<16>(a, grid, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st) {
+  if (p < 1 || p > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lm_chol_kernel, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(32 * NS), 0, st, part, nparts, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {

@@ -15,6 +15,9 @@ int pass_wg_per_cu(int P16);    // workgroups per CU the variant is built for
 bool pass_uses_split(int P16, int fused_split, int64_t ld);  // K1r (one 12-wave workgroup per CU) for this pass
 hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st);
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
+hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st);  // [nparts][NS] -> [NS]
+// LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}
+hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st);
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st);
 hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
                           double* out, hipStream_t st, const ProcX& g);

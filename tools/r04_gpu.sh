@@ -20,11 +20,24 @@ if [[ ,$STAGES, == *,ab,* ]]; then  # same-box A/B: the round-3 library (lib_ab/
   AN=125000000 AP=64 AK=2 AF=poisson AL=log timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p64.log 2>&1 || { echo "ab p64 failed"; tail gpurun_out/ab_p64.log; exit 1; }
   cat gpurun_out/ab_p32.log gpurun_out/ab_p64.log
 fi
+if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default head, tree) at p = 80 / 96 / 128
+  export AB_LIBS=${AB_MID_LIBS:-sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=2
+  for pn in "80 37500000" "96 31250000" "128 23437500"; do set -- $pn
+    AN=$2 AP=$1 AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py >> gpurun_out/ab_mid.log 2>&1 || { echo "ab mid failed"; tail gpurun_out/ab_mid.log; exit 1; }
+  done
+  cat gpurun_out/ab_mid.log
+fi
 if [[ ,$STAGES, == *,benchw,* ]]; then  # the other workloads' bench lines (WORKLOADS env: space-separated)
   for w in ${WORKLOADS:-poisson64}; do
     timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-load > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { echo "bench $w failed"; tail -20 gpurun_out/bench_$w.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/bench_$w.json')); r=d['roofline']; print('$w', d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], d['iters_to_converge'])"
   done
+fi
+if [[ ,$STAGES, == *,lm,* ]]; then  # configs[0] host overhead: wall per fit, then the kernel / copy timeline
+  timeout -k 10 300 python tools/lm_timeline.py 300 > gpurun_out/lm_timeline.log 2>&1 || { echo "lm timeline failed"; tail gpurun_out/lm_timeline.log; exit 1; }
+  cat gpurun_out/lm_timeline.log
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_lm" -o lm --output-format csv -- python tools/lm_timeline.py 100 > gpurun_out/prof_lm.log 2>&1 || { echo "lm prof failed"; tail gpurun_out/prof_lm.log; exit 1; }
 fi
 if [[ ,$STAGES, == *,rehearse8,* ]]; then  # 8 ranks sharing this GPU over gloo (the 8-GPU launch path)
   timeout -k 10 900 python bench.py --gpus 8 --rows 10000000 --steps 3 --warmup 1 --no-load > gpurun_out/bench_gpus8.json 2> gpurun_out/bench_gpus8.err || { echo "rehearsal failed"; tail -20 gpurun_out/bench_gpus8.err; exit 1; }

@@ -691,7 +691,7 @@ struct sglm_engine : public Backend {
       const int64_t need = (nblocks * RB + per_wg - 1) / per_wg;
       grid = (int)std::max<int64_t>(1, std::min(need, want_grid));
     } else {
-      if (!wide) P16 = pass_variant((int)p);
+      if (!wide) P16 = pass_variant((int)p, fused_split, n_pad);
       stride = wide ? 0 : pass_stride(P16);
       if (!wide) {
         const int64_t want_grid = (int64_t)ncu * (pass_uses_split(P16, fused_split, n_pad) ? 1 : pass_wg_per_cu(P16));
@@ -2186,7 +2186,7 @@ int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int f
   }
   const int64_t n_pad = (n + RB - 1) / RB * RB;  // alloc_data's leading dimension
   const bool proc = (flags & 1) != 0, wide = proc || (flags & 2) || p > 16 * MAX_P16, narrow = !wide && p <= 64;
-  const int P16 = wide ? 0 : narrow ? narrow_variant((int)p) : pass_variant((int)p);
+  const int P16 = wide ? 0 : narrow ? narrow_variant((int)p) : pass_variant((int)p, fused_split, n_pad);
   char buf[64];
   const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, family, link, buf, sizeof buf);
   if (name && namelen > 0) std::snprintf(name, (size_t)namelen, "%s", buf);

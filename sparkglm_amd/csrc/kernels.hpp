@@ -8,12 +8,13 @@
 
 namespace sglm {
 
-int pass_variant(int p);        // column-block count P16 of the kernel instantiated for p
-int pass_waves(int P16);        // waves per workgroup of that variant
+// column-block count P16 of the fused kernel a pass over p columns runs (odd: K1r only)
+int pass_variant(int p, int fused_split, int64_t ld);
 int pass_stride(int P16);       // doubles per workgroup partial
 int pass_wg_per_cu(int P16);    // workgroups per CU the variant is built for
 bool pass_uses_split(int P16, int fused_split, int64_t ld);  // K1r (one 12-wave workgroup per CU) for this pass
 hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st);
+hipError_t launch_pass_odd(int P16, const PassArgs& a, int grid, hipStream_t st);  // fused_odd.hip: K1r, P16 5..15 odd
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
 hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st);  // [nparts][NS] -> [NS]
 // LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}

@@ -5,12 +5,14 @@ created).
 At P16 = 16 (225 <= p <= 256) K1r accumulates every Gram tile and X'Wz column in K1's order (same
 k-steps, blocks and lanes) and its row stage is K1's, so one pass and a whole fit must come out
 BITWISE the same -- for every family / link and with offset + prior weights (the row stage's four
-vectors, staged by the four row waves), at p = 256 and at p = 232 (column quads past p are
+vectors, staged by the four row waves), at p = 256 and at p = 242 (column quads past p are
 duplicated into the padded LDS image), over shards that split into ragged row ranges per
 workgroup, and for a shard smaller than one row block per workgroup.
 
-Below P16 = 16 (the mid-width generalisation, K1r by default from P16 = 10) the Gram waves own other
-tile runs than K1's waves and the row stage reads another lane layout: NOT bitwise.  There both
+Below P16 = 16 (the mid-width generalisation, K1r by default from P16 = 10 and at every odd column-block
+count from 5: p = 65..80, 97..112, ..., 225..240 run ceil(p/16) blocks, where K1 runs the next even
+count) the Gram waves own other tile runs than K1's waves and the row stage reads another lane layout
+(and at odd counts the Gram itself is another tiling): NOT bitwise.  There both
 kernels are held to the oracle (partitionComponents / zwCreateBinomial, GLM.scala:359-395,
 utils.scala:84-92) at 1e-9 with the same iteration count, and to each other at 1e-12."""
 import os
@@ -38,8 +40,8 @@ def _engine(split: bool) -> Engine:
 CASES = [
     # (label, synth kind, rows, p, family, link)
     ("p256 logit", 0, 300_007, 256, "binomial", "logit"),
-    ("p232 probit", 0, 150_001, 232, "binomial", "probit"),
-    ("p240 cloglog", 0, 120_000, 240, "binomial", "cloglog"),
+    ("p242 probit", 0, 150_001, 242, "binomial", "probit"),
+    ("p248 cloglog", 0, 120_000, 248, "binomial", "cloglog"),
     ("p256 poisson + offset + prior", 2, 200_003, 256, "poisson", "log"),
     ("p250 gamma", 3, 100_000, 250, "gamma", "inverse"),
     ("p256 gaussian", 1, 90_000, 256, "gaussian", "identity"),
@@ -77,7 +79,13 @@ MID = [
     ("p150 poisson + offset + prior", 2, 120_001, 150, "poisson", "log", "1"),
     ("p200 gamma", 3, 60_000, 200, "gamma", "inverse", "1"),
     ("p180 logit, fewer blocks than workgroups", 0, 3_000, 180, "binomial", "logit", "1"),
-    ("p129 probit", 0, 90_000, 129, "binomial", "probit", "1"),
+    ("p129 probit (odd P16 = 9)", 0, 90_000, 129, "binomial", "probit", "1"),
+    ("p80 logit (odd P16 = 5)", 0, 150_000, 80, "binomial", "logit", "1"),
+    ("p70 poisson + offset + prior (odd P16 = 5, padded stripe)", 2, 100_003, 70, "poisson", "log", "1"),
+    ("p232 probit (odd P16 = 15)", 0, 90_001, 232, "binomial", "probit", "1"),
+    ("p240 gaussian (odd P16 = 15)", 1, 60_000, 240, "gaussian", "identity", "1"),
+    ("p105 gamma (odd P16 = 7)", 3, 60_000, 105, "gamma", "inverse", "1"),
+    ("p170 cloglog, few blocks (odd P16 = 11)", 0, 4_000, 170, "binomial", "cloglog", "1"),
     ("p96 cloglog, K1r forced from P16 = 6", 0, 100_000, 96, "binomial", "cloglog", "6"),
     ("p112 poisson + offset + prior, K1r forced from P16 = 6", 2, 80_000, 112, "poisson", "log", "6"),
 ]
@@ -126,14 +134,17 @@ def test_mid_width_k1r_and_k1_match_oracle(label, kind, n, p, family, link, thr)
     assert rel(a.stderr, b.stderr) < 1e-10 and rel(a.deviance, b.deviance) < 1e-12
 
 
-def test_p160_shard_reports_k1r():
+@pytest.mark.parametrize("p,name", [(160, "irls_pass_r_kernel<10,binomial,logit>"),
+                                    (80, "irls_pass_r_kernel<5,binomial,logit>")])
+def test_shard_reports_k1r(p, name):
     """The bench / roofline label comes from the engine's dispatch (sglm_stats.pass_kernel_name)."""
     with Engine(0) as e:
-        e.synth(0, 0, 50_000, 160, 3)
-        e.irls_pass(np.full(160, 0.01))
+        e.synth(0, 0, 50_000, p, 3)
+        e.irls_pass(np.full(p, 0.01))
         st = e.stats()
     assert st["pass_kernel_kind"] == "fused-split"
-    assert st["pass_kernel_name"] == "irls_pass_r_kernel<10,binomial,logit>"
+    assert st["pass_kernel_name"] == name
+    assert st["kernel_variant"] == int(name.split("<")[1].split(",")[0])
 
 
 def test_split_pass_matches_oracle():

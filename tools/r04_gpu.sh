@@ -20,10 +20,10 @@ if [[ ,$STAGES, == *,ab,* ]]; then  # same-box A/B: the round-3 library (lib_ab/
   AN=125000000 AP=64 AK=2 AF=poisson AL=log timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p64.log 2>&1 || { echo "ab p64 failed"; tail gpurun_out/ab_p64.log; exit 1; }
   cat gpurun_out/ab_p32.log gpurun_out/ab_p64.log
 fi
-if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default head, tree) at p = 80 / 96 / 128
+if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default head, tree) at p = 80 / 96 / 112 / 128 / 240
   export AB_LIBS=${AB_MID_LIBS:-sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=2
-  for pn in "80 37500000" "96 31250000" "128 23437500"; do set -- $pn
-    AN=$2 AP=$1 AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py >> gpurun_out/ab_mid.log 2>&1 || { echo "ab mid failed"; tail gpurun_out/ab_mid.log; exit 1; }
+  for pn in ${AB_MID_P:-80:37500000 96:31250000 112:26785714 128:23437500 240:10000000}; do
+    AN=${pn#*:} AP=${pn%:*} AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py >> gpurun_out/ab_mid.log 2>&1 || { echo "ab mid failed"; tail gpurun_out/ab_mid.log; exit 1; }
   done
   cat gpurun_out/ab_mid.log
 fi

@@ -1080,8 +1080,8 @@ struct sglm_engine : public Backend {
     a.eta_out = (mode == MODE_IRLS && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.fused_split = fused_split;
-    HIPCHK(hipEventRecord(ev0, st));
     if (wide) {
+      HIPCHK(hipEventRecord(ev0, st));
       WideRowArgs r{};
       r.X = dX;
       r.ld = n_pad;
@@ -1208,14 +1208,19 @@ struct sglm_engine : public Backend {
       HIPCHK(hipEventRecord(ev1, st));
       HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, drp, rgrid, dred, st));
     } else {
+      // the pass kernel and the reduce record ev0 / ev1 / ev2 as part of their dispatches
+      // (hipExtLaunchKernel): separate event records put a ~5 us marker between the kernels,
+      // a tenth of an LM.fit on configs[0]
       if (nblocks > 0) {
-        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st));
-        else HIPCHK(launch_pass(P16, a, grid, st));
+        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, ev0, ev1));
+        else HIPCHK(launch_pass(P16, a, grid, st, ev0, ev1));
       } else {
+        HIPCHK(hipEventRecord(ev0, st));
         HIPCHK(hipMemsetAsync(dpart, 0, sizeof(double) * stride, st));
+        HIPCHK(hipEventRecord(ev1, st));
       }
-      HIPCHK(hipEventRecord(ev1, st));
-      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st));
+      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st, ev2));
+      return SGLM_OK;
     }
     HIPCHK(hipEventRecord(ev2, st));
     return SGLM_OK;
@@ -1313,17 +1318,20 @@ struct sglm_engine : public Backend {
     if (!allow_lm_device || group() || comm.kind != 0 || wide || procx.on || !narrow || p > 64 || nblocks <= 0)
       return SGLM_OK;
     HIPCHK(hipSetDevice(device));
+    // one device buffer, copied back in one piece: packed Gram | residual statistics [NS] | coefs [p]
     const int64_t plen = packed_len(p);
-    if (int rc = ensure_red_len(plen)) return rc;
+    if (int rc = ensure_red_len(plen + NS + p)) return rc;
     if (int rc = ensure_small(64)) return rc;
     if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY)) return rc;
     double* aux = dsmall + NS;  // {ybar, leave-Cholesky flag}
-    HIPCHK(launch_lm_chol(dred, (int)p, LU_SWITCH_RATIO, dbeta, aux, st));
+    double* dstat = dred + plen;
+    double* dcoef = dred + plen + NS;
+    HIPCHK(launch_lm_chol(dred, (int)p, LU_SWITCH_RATIO, dcoef, aux, st));
     StatsArgs a{};
     a.X = dX;
     a.ld = n_pad;
     a.p = (int)p;
-    a.beta = dbeta;
+    a.beta = dcoef;
     a.ybar_dev = aux;
     a.y = dy;
     a.n = n;
@@ -1333,16 +1341,14 @@ struct sglm_engine : public Backend {
     a.partials = dpart;
     const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
     HIPCHK(launch_stats(a, nb, st));
-    HIPCHK(launch_reduce_stats(dpart, nb, dsmall, st));
-    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * plen, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(hsmall, dsmall, sizeof(double) * NS, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(hbeta, dbeta, sizeof(double) * p, hipMemcpyDeviceToHost, st));
+    HIPCHK(launch_reduce_stats(dpart, nb, dstat, st));
+    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * (plen + NS + p), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (int rc = pass_timing()) return rc;
     red_on_device = true;
     std::memcpy(packed, hred, sizeof(double) * plen);
-    std::memcpy(s, hsmall, sizeof(double) * NS);
-    std::memcpy(dev_coefs, hbeta, sizeof(double) * p);
+    std::memcpy(s, hred + plen, sizeof(double) * NS);
+    std::memcpy(dev_coefs, hred + plen + NS, sizeof(double) * p);
     done = true;
     lm_device_fits += 1;
     return SGLM_OK;

@@ -62,11 +62,10 @@ struct Geo {
   static constexpr int OFF_FLAG = OFF_INIT + 6;    // row-wave staging counter (uint32)
   static constexpr int LDS_DOUBLES = OFF_FLAG + 1;
   static constexpr int STRIDE = T * 256 + NC + NS; // partial stride (doubles)
-  // workgroups per CU: 8 waves per CU at least (2 per SIMD), LDS permitting
-#ifndef SGLM_EXP_WAVES
-#define SGLM_EXP_WAVES 8
-#endif
-  static constexpr int WMAX = SGLM_EXP_WAVES;  // EXPERIMENT (tools/ab.py): waves per CU wanted
+  // workgroups per CU: up to 12 waves per CU (3 per SIMD), LDS permitting -- P16 = 6 runs three
+  // 3-wave workgroups (8 waves wanted: two; same-box p = 96 pass 9.30 -> 8.57 ms, p = 80 10.73 ->
+  // 9.87 ms, no spills at the 168-VGPR budget); P16 >= 8 stays LDS-bound at two workgroups or one
+  static constexpr int WMAX = 12;
   static constexpr int WG_PER_CU = (WMAX / NW) * (LDS_DOUBLES * 8) <= 160 * 1024 ? WMAX / NW : 160 * 1024 / (LDS_DOUBLES * 8);
   static constexpr int WAVES_PER_SIMD = (WG_PER_CU * NW + 3) / 4;
   // Block rows of wave wv's tiles: HI = P16-1-wv and LO below.  The row waves carry the row
@@ -511,17 +510,33 @@ struct TilesR {
   static_assert(P16 == 16 || ROW || row(NSEG) < 0 || true, "segments");
 };
 
+// K1r's LDS: a ring of NBUF row-block buffers -- as deep as 160 KB allows (4 up to P16 = 8, 3 up to
+// 12, 2 above): the DMA of block b + NBUF is issued when block b is consumed, so a row wave finds the
+// next block landed instead of waiting out its HBM latency (with two buffers that latency plus the
+// row stage was the per-block critical path whenever the Gram of a block is short, i.e. below P16 ~ 10).
 template <int P16>
 struct GeoR {
   using G = Geo<P16>;
   static constexpr int NW = 12, NGW = 8;
-  static constexpr int OFF_RED = G::OFF_RED;              // [NW][NS]
-  // [8 lane groups][4 NCE/32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
+  static constexpr int XB = G::XB;                        // doubles per X buffer (K1's image)
   static constexpr int BETAG_STRIDE = 34;
+  static constexpr int PER_BUF = XB + 4 * RB + 2 * RB + RB;  // X | y, m, offset, prior | w, w*z | eta
+  static constexpr int FIXED = G::NCE + NW * NS + 8 * BETAG_STRIDE + 2 + 6;
+  static constexpr int LDS_MAX = 160 * 1024 / 8;
+  static constexpr int NBUF = 4 * PER_BUF + FIXED <= LDS_MAX ? 4 : (3 * PER_BUF + FIXED <= LDS_MAX ? 3 : 2);
+  static constexpr int OFF_X = 0;                         // [NBUF][XB]
+  static constexpr int OFF_V = NBUF * XB;                 // [NBUF][4][RB]
+  static constexpr int OFF_W = OFF_V + NBUF * 4 * RB;     // [NBUF][w RB | w*z RB]
+  static constexpr int OFF_ETA = OFF_W + NBUF * 2 * RB;   // [NBUF][RB] the row stage's eta (stored by Gram wave 0)
+  static constexpr int OFF_BETA = OFF_ETA + NBUF * RB;    // [NCE]
+  static constexpr int OFF_RED = OFF_BETA + G::NCE;       // [NW][NS]
+  // [8 lane groups][4 NCE/32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
   static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas
   static constexpr int OFF_FLAG = OFF_BETAG + 8 * BETAG_STRIDE;        // counters: row-wave staging, ready, done (uint32)
   static constexpr int OFF_INIT = OFF_FLAG + 2;                         // [6] init_const
   static constexpr int LDS_DOUBLES = OFF_INIT + 6;
+  static_assert(LDS_DOUBLES == NBUF * PER_BUF + FIXED, "layout");
+  static_assert(XB % 2 == 0 && OFF_V % 2 == 0, "LDS-DMA destinations 16-byte aligned");
   static constexpr int QPW = P16;                         // column quads each row wave stages
   static constexpr int NT = G::NCE / 32;                  // 32-column stripes of the row stage
   static_assert(LDS_DOUBLES * 8 <= 160 * 1024, "LDS");
@@ -548,9 +563,10 @@ struct XzBlocks {
 template <int P16, int K>
 __device__ __forceinline__ void xz_rows_r(const double* lds, int buf, int lane, double (&xz)[4]) {
   using G = Geo<P16>;
+  using R = GeoR<P16>;
   using XB = XzBlocks<P16, K>;
-  const double* xs = lds + G::OFF_X + buf * G::XB + XB::LO * G::BSTR;
-  const double* wz = lds + G::OFF_W + buf * 2 * RB + RB;
+  const double* xs = lds + R::OFF_X + buf * R::XB + XB::LO * G::BSTR;
+  const double* wz = lds + R::OFF_W + buf * 2 * RB + RB;
   const int cl = lane & 15, rq = lane >> 4;
   const double* colbase = xs + cl * 32;
   // two LDS round trips (every read of a half issued before its first FMA: a round trip of a row
@@ -586,7 +602,7 @@ __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassAr
   using G = Geo<P16>;
   typedef __attribute__((address_space(3))) double lds_double;
   lds_double* l3 = (lds_double*)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(lds_void*)lds);
-  lds_double* xdst = l3 + G::OFF_X + buf * G::XB;
+  lds_double* xdst = l3 + GeoR<P16>::OFF_X + buf * GeoR<P16>::XB;
   const int64_t r0 = blk * RB;
   const int q0 = si * GeoR<P16>::QPW;
 #pragma unroll
@@ -603,7 +619,8 @@ __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassAr
   if (si == 3 && a.prior) src = a.prior;
   const char* sb = (const char*)(src + r0);
   if ((int)vvoff < 16 * 16)
-    __builtin_amdgcn_global_load_lds((const void*)(sb + vvoff), (lds_void*)(l3 + G::OFF_V + buf * 4 * RB + si * RB), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vvoff), (lds_void*)(l3 + GeoR<P16>::OFF_V + buf * 4 * RB + si * RB), 16,
+                                     0, 0);
 }
 
 // Row stage of K1r: K1's row_stage (the same lanes, partial sums and reduction order, so w, w*z
@@ -617,11 +634,12 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
   using G = Geo<P16>;
   constexpr int RW = 8, CPG = 4, NT = GeoR<P16>::NT;
   static_assert(P16 != 16 || (G::RW == RW && G::CPG == CPG && NT == 8), "K1's P16 = 16 row-stage geometry");
-  const double* xs = lds + G::OFF_X + buf * G::XB;
+  using R = GeoR<P16>;
+  const double* xs = lds + R::OFF_X + buf * R::XB;
   const int rl = lane % RW, g = lane / RW;
-  const double* bg = lds + GeoR<P16>::OFF_BETAG + g * GeoR<P16>::BETAG_STRIDE;
+  const double* bg = lds + R::OFF_BETAG + g * R::BETAG_STRIDE;
   const int r = RW * rw + rl;
-  const double* vv = lds + G::OFF_V + buf * 4 * RB;
+  const double* vv = lds + R::OFF_V + buf * 4 * RB;
   const double y = vv[r];
   const double m = a.m ? vv[RB + r] : 1.0;
   const double off = a.off ? vv[2 * RB + r] : 0.0;
@@ -659,16 +677,16 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
     const int64_t row = blk * RB + r;
     double w = 0.0, wz = 0.0;
     if (row < a.n) {
-      if (a.mode == MODE_IRLS) {
-        eta = eta + off;
-        if (a.eta_out) a.eta_out[row] = eta;
-      }
+      if (a.mode == MODE_IRLS) eta = eta + off;
       if (FAM == FAM_BINOMIAL && init_fast_row(FAM, a.mode, a.m != nullptr) && y >= 0.0 && y <= 1.0)
-        pass_row_init(lds + GeoR<P16>::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
+        pass_row_init(lds + R::OFF_INIT, y, off, pw, w, wz, s_dev, s_aux);
       else pass_row(FAM, LNK, a.mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true);
     }
-    lds[G::OFF_W + buf * 2 * RB + r] = w;
-    lds[G::OFF_W + buf * 2 * RB + RB + r] = wz;
+    lds[R::OFF_W + buf * 2 * RB + r] = w;
+    lds[R::OFF_W + buf * 2 * RB + RB + r] = wz;
+    // eta leaves through LDS: Gram wave 0 stores it after the block's Gram, so the row waves' only
+    // vector-memory operations are their LDS-DMA and vmcnt counts exactly the blocks in flight
+    lds[R::OFF_ETA + buf * RB + r] = eta;
   }
 }
 
@@ -676,8 +694,8 @@ template <int P16, int WV>
 __device__ __forceinline__ void gram_steps_r(const double* lds, int buf, int lane, d4 (&acc)[TilesR<P16, WV>::NT]) {
   using G = Geo<P16>;
   using T = TilesR<P16, WV>;
-  const double* xs = lds + G::OFF_X + buf * G::XB;
-  const double* w = lds + G::OFF_W + buf * 2 * RB;
+  const double* xs = lds + GeoR<P16>::OFF_X + buf * GeoR<P16>::XB;
+  const double* w = lds + GeoR<P16>::OFF_W + buf * 2 * RB;
   const int cl = lane & 15, rq = lane >> 4;
   const double* colbase = xs + cl * 32;
   auto kstep = [&](int j) {
@@ -742,21 +760,31 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
 #pragma unroll
   for (int k = 0; k < 4; ++k) voff[k] = (uint32_t)(((int64_t)lcq * a.ld + ((2 * li) ^ ((8 * k + 2 * lcq) & 31))) * 8);
   const uint32_t vvoff = (uint32_t)(lane < 16 ? 16 * lane : 16 * 16);
-  if (row_wave && b0 < b1) {
-    stage_block_r<P16>(lds, 0, a, b0, si, voff, vvoff);
-    if (b0 + 1 < b1) stage_block_r<P16>(lds, 1, a, b0 + 1, si, voff, vvoff);
-  }
+  constexpr int NB = R::NBUF, PER = R::QPW + 1;  // ring depth; vector-memory operations per staged block
+  if (row_wave)
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (b0 + k < b1) stage_block_r<P16>(lds, k, a, b0 + k, si, voff, vvoff);
   if (row_wave) __builtin_amdgcn_s_setprio(2);
-  // No block barrier: three LDS counters order the ring of two buffers.
+  // wait until this wave's DMA of a block has landed while `later` blocks staged after it may fly
+  auto wait_landed = [&](int64_t later) {
+    if constexpr (NB >= 4)
+      if (later >= 3) return wait_vmcnt<3 * PER>();
+    if constexpr (NB >= 3)
+      if (later >= 2) return wait_vmcnt<2 * PER>();
+    if (later >= 1) return wait_vmcnt<PER>();
+    wait_vmcnt<0>();
+  };
+  // No block barrier: three LDS counters order the ring of NBUF buffers.
   //   flag : +1 per row wave when its LDS-DMA part of a block has landed (4 per block)
   //   ready: +1 per row wave when its rows of a block's row stage are in the w buffer (4 per block)
   //   done : +1 per wave when it has finished reading a block: the Gram waves' MFMAs, the row
   //          waves' X'Wz (12 per block)
   // A Gram wave starts block b once ready(b) and may run up to one block ahead of the slowest
   // Gram wave, so the two Gram waves of a SIMD no longer end every block with one of them alone
-  // on the MFMA pipe; the row waves stage block b+2 into block b's buffers after done(b).
-  // (The row stage of b+2 rewrites w(b): the flag round of b+2 orders it after every row wave's
-  // X'Wz of b.)
+  // on the MFMA pipe; the row waves stage block b+NBUF into block b's buffers after done(b).
+  // (The row stage of b+NBUF rewrites w(b): it follows that row wave's own wait for done(b), and its
+  // flag round orders it after every row wave's DMA of b+NBUF.)
   unsigned* ready = flag + 1;
   unsigned* done = flag + 2;
   auto spin = [&](unsigned* c, unsigned target) {
@@ -765,23 +793,23 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   auto bump = [&](unsigned* c) {
     if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
+  auto next_buf = [](int b) { return b + 1 == NB ? 0 : b + 1; };
   if constexpr (row_wave) {
     if (b0 < b1) {
-      if (b0 + 1 < b1) wait_vmcnt<R::QPW + 1>();
-      else wait_vmcnt<0>();
+      wait_landed(std::min<int64_t>(b1 - b0 - 1, NB - 1));
       bump(flag);
       spin(flag, 4u);
       row_stage_r<P16, FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
       bump(ready);
     }
+    int cur = 0;
 #pragma unroll 1
-    for (int64_t blk = b0; blk < b1; ++blk) {
-      const int cur = (int)((blk - b0) & 1);
+    for (int64_t blk = b0; blk < b1; ++blk, cur = next_buf(cur)) {
       if (blk + 1 < b1) {
-        wait_vmcnt<0>();
+        wait_landed(std::min<int64_t>(b1 - blk - 2, NB - 2));
         bump(flag);
         spin(flag, (unsigned)(4 * (blk + 2 - b0)));
-        row_stage_r<P16, FAM, LNK>(lds, cur ^ 1, a, blk + 1, si, lane, s_dev, s_aux);
+        row_stage_r<P16, FAM, LNK>(lds, next_buf(cur), a, blk + 1, si, lane, s_dev, s_aux);
         bump(ready);
       }
       // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them
@@ -789,17 +817,20 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
       if (blk + 1 >= b1) spin(ready, (unsigned)(4 * (blk - b0 + 1)));
       if (do_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
       bump(done);  // this row wave's reads of block blk (X'Wz) are complete
-      if (blk + 2 < b1) {
+      if (blk + NB < b1) {
         spin(done, (unsigned)(12 * (blk - b0 + 1)));
-        stage_block_r<P16>(lds, cur, a, blk + 2, si, voff, vvoff);
+        stage_block_r<P16>(lds, cur, a, blk + NB, si, voff, vvoff);
       }
     }
   } else {
+    int cur = 0;
 #pragma unroll 1
-    for (int64_t blk = b0; blk < b1; ++blk) {
-      const int cur = (int)((blk - b0) & 1);
+    for (int64_t blk = b0; blk < b1; ++blk, cur = next_buf(cur)) {
       spin(ready, (unsigned)(4 * (blk - b0 + 1)));
       if (do_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
+      if constexpr (WV == 0)  // the row stage's eta of this block (IRLS passes that keep it)
+        if (a.eta_out && a.mode == MODE_IRLS && lane < RB && blk * RB + lane < a.n)
+          a.eta_out[blk * RB + lane] = lds[R::OFF_ETA + cur * RB + lane];
       bump(done);
     }
   }
@@ -858,7 +889,7 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int c = threadIdx.x; c < G::NCE; c += 64 * R::NW) {
     const double b = (a.beta && c < a.p) ? a.beta[c] : 0.0;
-    lds[G::OFF_BETA + c] = b;
+    lds[R::OFF_BETA + c] = b;
     // betag[g][t * 4 + u] = beta[4 g + u + 32 t] (row_stage_r)
     lds[R::OFF_BETAG + ((c & 31) >> 2) * R::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
   }
@@ -866,8 +897,8 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
   if constexpr (G::NCE > G::NC) {  // odd P16: the row stage's last stripe reads 16 columns no DMA writes
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * R::NW) {
       const int c = G::NC + e / RB, r = e % RB;
-      lds[G::OFF_X + (c >> 4) * G::BSTR + (c & 15) * RB + r] = 0.0;
-      lds[G::OFF_X + G::XB + (c >> 4) * G::BSTR + (c & 15) * RB + r] = 0.0;
+#pragma unroll
+      for (int k = 0; k < R::NBUF; ++k) lds[R::OFF_X + k * R::XB + (c >> 4) * G::BSTR + (c & 15) * RB + r] = 0.0;
     }
   }
   if constexpr (FAM == FAM_BINOMIAL)
@@ -894,16 +925,16 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
 
 // K1r launch for the family/link of the pass (LM passes: the Gaussian identity row stage).
 template <int P16>
-static hipError_t launch_pass_r_fl(const PassArgs& a, int grid, hipStream_t st) {
+static hipError_t launch_pass_r_fl(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   const dim3 g(grid), b(64 * GeoR<P16>::NW);
-  if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
-  else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, a);
-  else if (fam == FAM_BINOMIAL) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, a);
-  else if (fam == FAM_GAUSSIAN) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, a);
-  else if (fam == FAM_POISSON) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, a);
-  else if (fam == FAM_GAMMA) hipLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, a);
+  if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, e0, e1, 0, a);
+  else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, e0, e1, 0, a);
+  else if (fam == FAM_BINOMIAL) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, e0, e1, 0, a);
+  else if (fam == FAM_GAUSSIAN) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, e0, e1, 0, a);
+  else if (fam == FAM_POISSON) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, e0, e1, 0, a);
+  else if (fam == FAM_GAMMA) hipExtLaunchKernelGGL((irls_pass_r_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, e0, e1, 0, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

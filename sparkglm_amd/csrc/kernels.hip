@@ -188,70 +188,80 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // LM.fit's p x p solve on the device (engine.cpp lm_device; p <= 64): the host solver's Cholesky
 // (solve.cpp chol_factor + chol_solve), element for element in the same operation order without
 // contraction, so the coefficients come out bitwise the host's (driver.cpp lm_drive checks that and
-// otherwise reruns the residual pass at its own).  Lane i owns row i: every column update is
-// lane-parallel with each element's subtractions in the host's k order; the back substitution's
-// dependent sums run on lane 0 in the host's order.  Out: beta[p]; aux[0] = sum y / rows (LM.scala:
-// 167-168), aux[1] = 1 where the host would leave Cholesky (a non-positive pivot, or the pivot
-// ratio below LU_SWITCH_RATIO: solve.cpp chol_pivot_ratio).
+// otherwise reruns the residual pass at its own).  Lane i owns row i.  The factorization runs
+// right-looking: step k takes column k's pivot, scales it, then subtracts L(i,k) L(j,k) from every
+// trailing element (i, j) -- each element still receives its subtractions in ascending k, exactly
+// chol_factor's left-looking order, but the subtractions of one step are independent (no dependent
+// chain of length j per column, which made the first, left-looking form 40K cycles at p = 20).
+// Both triangular solves are column sweeps: the pivot's quotient on its lane, handed to the others
+// by readlane.  Out: beta[p]; aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where the host
+// would leave Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO:
+// solve.cpp chol_pivot_ratio).
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
                                                      double* __restrict__ beta, double* __restrict__ aux) {
 #pragma clang fp contract(off)
-  __shared__ double A[64 * 64], dg[64], t[64];
+  constexpr int LD = 65, U = 8;  // A(r, c) at A[c LD + r]: column reads by lane conflict-free, row reads 2-way
+  __shared__ double A[64 * LD], dg[64];
   const int i = threadIdx.x;
+  const bool row = i < p;
   const int64_t tri = (int64_t)p * (p + 1) / 2;
   for (int e = i; e < p * p; e += 64) {  // unpack_gram: A(r, c) = packed[max(r, c) (max + 1) / 2 + min(r, c)]
     const int r = e % p, c = e / p, hi = r > c ? r : c, lo = r > c ? c : r;
-    A[e] = packed[hi * (hi + 1) / 2 + lo];
+    A[c * LD + r] = packed[hi * (hi + 1) / 2 + lo];
   }
-  if (i < p) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
+  if (row) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
+  double ti = row ? packed[tri + i] : 0.0;
   __syncthreads();
   int fail = 0;
-  for (int j = 0; j < p; ++j) {  // chol_factor (left-looking jki)
-    double aj = (i < p) ? A[i + j * p] : 0.0;
-    for (int k = 0; k < j; ++k) {
-      const double ljk = A[j + k * p];
-      if (ljk == 0.0) continue;
-      if (i >= j && i < p) aj -= A[i + k * p] * ljk;
-    }
-    if (i >= j && i < p) A[i + j * p] = aj;
-    __syncthreads();
-    const double d = A[j + j * p];
+  for (int k = 0; k < p; ++k) {  // chol_factor
+    const double d = A[k * LD + k];
+    const double aik = A[k * LD + i];
     if (!(d > 0.0) || !isfinite(d)) {
       fail = 1;
       break;
     }
-    const double s = sqrt(d);
-    const double inv = 1.0 / s;
+    const double sq = sqrt(d);
+    const double inv = 1.0 / sq;
+    const double lik = (i == k) ? sq : aik * inv;  // L(i, k), lanes i >= k
+    if (i >= k && row) A[k * LD + i] = lik;
     __syncthreads();
-    if (i == j) A[j + j * p] = s;
-    if (i > j && i < p) A[i + j * p] = aj * inv;
-    __syncthreads();
-  }
-  double ti = 0.0;
-  if (!fail) {
-    ti = (i < p) ? packed[tri + i] : 0.0;  // chol_solve: L t = b, column sweep
-    for (int j = 0; j < p; ++j) {
-      if (i == j) t[j] = ti / A[j + j * p];
-      __syncthreads();
-      const double tj = t[j];
-      if (i == j) ti = tj;
-      if (i > j && i < p) ti -= A[i + j * p] * tj;
-    }
-    if (i == 0) {  // L' x = t, dependent sums in the host's order
-      for (int r = p - 1; r >= 0; --r) {
-        double s = t[r];
-        for (int k = r + 1; k < p; ++k) s -= A[k + r * p] * t[k];
-        t[r] = s / A[r + r * p];
+    for (int j0 = k + 1; j0 < p; j0 += U) {  // A(i, j) -= L(i, k) L(j, k), j = k+1 .. i; L(j, k) == 0 skipped
+      double l[U], x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u < p ? j0 + u : p - 1;
+        l[u] = A[k * LD + j];
+        x[u] = A[j * LD + i];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u;
+        if (j < p && i >= j && row && l[u] != 0.0) A[j * LD + i] = x[u] - lik * l[u];
       }
     }
     __syncthreads();
-    if (i < p) beta[i] = t[i];
+  }
+  if (!fail) {
+    for (int j = 0; j < p; ++j) {  // L t = b: t_j /= L(j, j); t_i -= L(i, j) t_j, i > j
+      const double tj = lane_bcast(ti / A[i * LD + i], j);
+      if (i == j) ti = tj;
+      if (i > j && row) ti -= A[j * LD + i] * tj;
+    }
+    for (int r = p - 1; r >= 0; --r) {  // L' x = t: x_r = t_r / L(r, r); t_i -= L(r, i) x_r, i < r
+      const double xr = lane_bcast(ti / A[i * LD + i], r);
+      if (i == r) ti = xr;
+      if (i < r) ti -= A[i * LD + r] * xr;
+    }
+    if (row) beta[i] = ti;
   }
   if (i == 0) {
     double r = 1.0;  // chol_pivot_ratio
     if (!fail)
       for (int j = 0; j < p; ++j) {
-        const double l = A[j + j * p], a = dg[j];
+        const double l = A[j * LD + j], a = dg[j];
         if (a > 0.0) r = fmin(r, (l * l) / a);
       }
     aux[0] = packed[tri + p + S_DEV] / packed[tri + p + S_SUMW];
@@ -268,7 +278,15 @@ __global__ void __launch_bounds__(256) reduce_stats_kernel(const double* __restr
   const int k = threadIdx.x % NS, sg = threadIdx.x / NS;
   const int g0 = (int)((int64_t)nparts * sg / 32), g1 = (int)((int64_t)nparts * (sg + 1) / 32);
   double s = 0.0, c = 0.0;
-  for (int g = g0; g < g1; ++g) neumaier_add(s, c, part[(int64_t)g * NS + k]);
+  int g = g0;
+  for (; g + 8 <= g1; g += 8) {  // 8 loads in flight ahead of the ordered compensated adds
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(g + u) * NS + k];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) neumaier_add(s, c, v[u]);
+  }
+  for (; g < g1; ++g) neumaier_add(s, c, part[(int64_t)g * NS + k]);
   ss[sg][k] = s;
   cs[sg][k] = c;
   __syncthreads();
@@ -327,13 +345,16 @@ __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t 
 // ---------------------------------------------------------------------------------
 // Kernel variants: P16 = ceil(p / 16) column blocks of 16 in 2..16 (p <= 256).  K1 is built for
 // even P16 (NW = P16/2 waves, two tile rows each); K1r for every P16 >= 5.  An odd count runs K1r
-// when the pass may (pass_uses_split) and is rounded up to K1's even count otherwise -- so p = 80
-// runs 15 tiles of 16 x 16 per k-step instead of 21 (the padded columns' MFMAs are 1/3 of P16 = 6).
-// K1r runs P16 >= the threshold PassArgs::fused_split carries (1: the default K1R_MIN_P16 for even
-// counts, K1R_MIN_ODD for odd ones; 0: never) -- one 12-wave workgroup per CU; K1 the rest.  Its
-// DMA addresses the 4 columns of a quad by 32-bit lane offsets (3 ld + 32 rows, in bytes), which
-// bounds the shard at ~178M rows.
-constexpr int K1R_MIN_P16 = 10, K1R_MIN_ODD = 5;
+// when the pass may (pass_uses_split) and is rounded up to K1's even count otherwise -- so p = 240
+// runs 120 tiles of 16 x 16 per k-step instead of 136.
+// K1r runs P16 >= the threshold PassArgs::fused_split carries (1: the default, K1R_MIN_P16 for even
+// counts and K1R_MIN_ODD for odd ones; 0: never) -- one 12-wave workgroup per CU; K1 the rest.
+// Same-box A/B (profiles/r04_midp_ab.txt): p = 240 K1r<15> 10.39 ms against K1r<16> 10.91 and K1<16>
+// 11.55; but p = 80 K1r<5> 10.25 against K1<6> at three workgroups per CU 9.87, p = 112 K1r<7> 10.37
+// against K1<8> 9.78-10.33 -- below P16 = 9 the eight Gram waves carry two to three tiles each.
+// Its DMA addresses the 4 columns of a quad by 32-bit lane offsets (3 ld + 32 rows, in bytes),
+// which bounds the shard at ~178M rows.
+constexpr int K1R_MIN_P16 = 10, K1R_MIN_ODD = 9;
 bool pass_uses_split(int P16, int fused_split, int64_t ld) {
   const int thr = fused_split == 1 ? ((P16 & 1) ? K1R_MIN_ODD : K1R_MIN_P16) : fused_split;
   return fused_split != 0 && P16 >= 5 && P16 >= thr && ld * 24 + 4096 < ((int64_t)1 << 32);
@@ -363,45 +384,45 @@ int pass_wg_per_cu(int P16) {
 }
 
 template <int P16>
-static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st) {
+static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   static_assert(P16 % 2 == 0, "K1: even column-block counts (odd ones: fused_odd.hip)");
   if constexpr (P16 >= 6)
-    if (pass_uses_split(P16, a.fused_split, a.ld)) return launch_pass_r_fl<P16>(a, grid, st);
+    if (pass_uses_split(P16, a.fused_split, a.ld)) return launch_pass_r_fl<P16>(a, grid, st, e0, e1);
   const dim3 g(grid), b(64 * Geo<P16>::NW);
   const int mode_fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int mode_lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, e0, e1, 0, a);
   else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, e0, e1, 0, a);
   else if (mode_fam == FAM_BINOMIAL)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, e0, e1, 0, a);
   else if (mode_fam == FAM_GAUSSIAN)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, e0, e1, 0, a);
   else if (mode_fam == FAM_POISSON)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, e0, e1, 0, a);
   else if (mode_fam == FAM_GAMMA)
-    hipLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, a);
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, e0, e1, 0, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st) {
+hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   if ((P16 & 1) && P16 >= 5) {
     // odd counts exist only as K1r: refuse a pass that may not run it (pass_variant rounds those up)
     if (!pass_uses_split(P16, a.fused_split, a.ld)) return hipErrorInvalidValue;
-    return launch_pass_odd(P16, a, grid, st);
+    return launch_pass_odd(P16, a, grid, st, e0, e1);
   }
   switch (P16) {
-    case 2: return launch_pass_p<2>(a, grid, st);
-    case 4: return launch_pass_p<4>(a, grid, st);
-    case 6: return launch_pass_p<6>(a, grid, st);
-    case 8: return launch_pass_p<8>(a, grid, st);
-    case 10: return launch_pass_p<10>(a, grid, st);
-    case 12: return launch_pass_p<12>(a, grid, st);
-    case 14: return launch_pass_p<14>(a, grid, st);
-    case 16: return launch_pass_p<16>(a, grid, st);
+    case 2: return launch_pass_p<2>(a, grid, st, e0, e1);
+    case 4: return launch_pass_p<4>(a, grid, st, e0, e1);
+    case 6: return launch_pass_p<6>(a, grid, st, e0, e1);
+    case 8: return launch_pass_p<8>(a, grid, st, e0, e1);
+    case 10: return launch_pass_p<10>(a, grid, st, e0, e1);
+    case 12: return launch_pass_p<12>(a, grid, st, e0, e1);
+    case 14: return launch_pass_p<14>(a, grid, st, e0, e1);
+    case 16: return launch_pass_p<16>(a, grid, st, e0, e1);
     default: return hipErrorInvalidValue;
   }
 }
@@ -436,11 +457,13 @@ hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st) {
+hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st,
+                         hipEvent_t e1) {
   const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
   int blocks = (int)((total + RED_EL - 1) / RED_EL);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks), dim3(256), 0, st, part, stride, nparts, p, P16, out);
+  hipExtLaunchKernelGGL(reduce_partials_kernel, dim3(blocks), dim3(256), 0, st, nullptr, e1, 0, part, stride, nparts, p, P16,
+                        out);
   return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 // kernels.hpp -- host-side launchers of the gfx950 kernels (kernels.hip).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -13,13 +14,17 @@ int pass_variant(int p, int fused_split, int64_t ld);
 int pass_stride(int P16);       // doubles per workgroup partial
 int pass_wg_per_cu(int P16);    // workgroups per CU the variant is built for
 bool pass_uses_split(int P16, int fused_split, int64_t ld);  // K1r (one 12-wave workgroup per CU) for this pass
-hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st);
-hipError_t launch_pass_odd(int P16, const PassArgs& a, int grid, hipStream_t st);  // fused_odd.hip: K1r, P16 5..15 odd
+// e0 / e1: HIP events the launch itself records at the kernel's start / end (hipExtLaunchKernel: no
+// marker packets between the kernels of a pass; null = none)
+hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0 = nullptr,
+                       hipEvent_t e1 = nullptr);
+hipError_t launch_pass_odd(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1);  // fused_odd.hip: K1r, P16 5..15 odd
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
 hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st);  // [nparts][NS] -> [NS]
 // LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}
 hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st);
-hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st);
+hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st,
+                         hipEvent_t e1 = nullptr);
 hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
                           double* out, hipStream_t st, const ProcX& g);
 hipError_t launch_unlink(double* v, const double* m, int64_t n, int family, int link, hipStream_t st);
@@ -33,7 +38,8 @@ int narrow_variant(int p);      // column blocks of 16 (1..4)
 int narrow_stride(int P16);     // doubles per workgroup partial (reduce_partials_kernel layout)
 int narrow_wg_per_cu();
 int narrow_rows_per_wg(int P16); // rows one workgroup streams per block step (waves x rows per block)
-hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st);
+hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0 = nullptr,
+                         hipEvent_t e1 = nullptr);
 
 // wide path (wide.hip)
 int wide_panels(int p);

@@ -508,33 +508,33 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 }
 
 template <int P16, int FAM, int LNK>
-void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st) {
+void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   constexpr bool SP = stats_in_pass_family(FAM, LNK);
   if (a.mode == MODE_IRLS && SP && a.stats_in_pass && !(FAM == FAM_BINOMIAL && a.m))
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, SP>), gr, bl, 0, st, a);
+    hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, SP>), gr, bl, 0, st, e0, e1, 0, a);
   else if (a.mode == MODE_IRLS)
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true>), gr, bl, 0, st, a);
+    hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true>), gr, bl, 0, st, e0, e1, 0, a);
   else
-    hipLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false>), gr, bl, 0, st, a);
+    hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false>), gr, bl, 0, st, e0, e1, 0, a);
 }
 
 template <int P16>
-hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st) {
+hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const dim3 gr(grid), bl(64 * NGeo<P16>::NW);
   const int fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
   const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   if (fam == FAM_BINOMIAL && lnk == LNK_LOGIT)
-    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_LOGIT>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_LOGIT>(a, gr, bl, st, e0, e1);
   else if (fam == FAM_BINOMIAL && lnk == LNK_PROBIT)
-    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_PROBIT>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_PROBIT>(a, gr, bl, st, e0, e1);
   else if (fam == FAM_BINOMIAL)
-    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_CLOGLOG>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_BINOMIAL, LNK_CLOGLOG>(a, gr, bl, st, e0, e1);
   else if (fam == FAM_GAUSSIAN)
-    launch_narrow_fl<P16, FAM_GAUSSIAN, LNK_IDENTITY>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_GAUSSIAN, LNK_IDENTITY>(a, gr, bl, st, e0, e1);
   else if (fam == FAM_POISSON)
-    launch_narrow_fl<P16, FAM_POISSON, LNK_LOG>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_POISSON, LNK_LOG>(a, gr, bl, st, e0, e1);
   else if (fam == FAM_GAMMA)
-    launch_narrow_fl<P16, FAM_GAMMA, LNK_INVERSE>(a, gr, bl, st);
+    launch_narrow_fl<P16, FAM_GAMMA, LNK_INVERSE>(a, gr, bl, st, e0, e1);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -554,12 +554,12 @@ int narrow_rows_per_wg(int P16) {
   }
 }
 
-hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st) {
+hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   switch (P16) {
-    case 1: return launch_narrow_p<1>(a, grid, st);
-    case 2: return launch_narrow_p<2>(a, grid, st);
-    case 3: return launch_narrow_p<3>(a, grid, st);
-    case 4: return launch_narrow_p<4>(a, grid, st);
+    case 1: return launch_narrow_p<1>(a, grid, st, e0, e1);
+    case 2: return launch_narrow_p<2>(a, grid, st, e0, e1);
+    case 3: return launch_narrow_p<3>(a, grid, st, e0, e1);
+    case 4: return launch_narrow_p<4>(a, grid, st, e0, e1);
     default: return hipErrorInvalidValue;
   }
 }

@@ -47,11 +47,10 @@ void chol_solve(const double* L, int64_t p, const double* b, double* x) {
     const double tj = t[j];
     for (int64_t i = j + 1; i < p; ++i) t[i] -= L[i + j * p] * tj;
   }
-  for (int64_t i = p - 1; i >= 0; --i) {  // L' x = t
-    double s = t[i];
-    const double* Li = L + i * p;
-    for (int64_t k = i + 1; k < p; ++k) s -= Li[k] * t[k];
-    t[i] = s / L[i + i * p];
+  for (int64_t i = p - 1; i >= 0; --i) {  // L' x = t (column sweep: x_i, then t_k -= L(i, k) x_i, k < i)
+    t[i] /= L[i + i * p];
+    const double xi = t[i];
+    for (int64_t k = 0; k < i; ++k) t[k] -= L[i + k * p] * xi;
   }
   std::memcpy(x, t.data(), sizeof(double) * p);
 }

@@ -10,8 +10,8 @@ duplicated into the padded LDS image), over shards that split into ragged row ra
 workgroup, and for a shard smaller than one row block per workgroup.
 
 Below P16 = 16 (the mid-width generalisation, K1r by default from P16 = 10 and at every odd column-block
-count from 5: p = 65..80, 97..112, ..., 225..240 run ceil(p/16) blocks, where K1 runs the next even
-count) the Gram waves own other tile runs than K1's waves and the row stage reads another lane layout
+count from 9: p = 129..144, ..., 225..240 run ceil(p/16) blocks, where K1 runs the next even count;
+odd 5 and 7 by SGLM_FUSED_SPLIT) the Gram waves own other tile runs than K1's waves and the row stage reads another lane layout
 (and at odd counts the Gram itself is another tiling): NOT bitwise.  There both
 kernels are held to the oracle (partitionComponents / zwCreateBinomial, GLM.scala:359-395,
 utils.scala:84-92) at 1e-9 with the same iteration count, and to each other at 1e-12."""
@@ -80,11 +80,11 @@ MID = [
     ("p200 gamma", 3, 60_000, 200, "gamma", "inverse", "1"),
     ("p180 logit, fewer blocks than workgroups", 0, 3_000, 180, "binomial", "logit", "1"),
     ("p129 probit (odd P16 = 9)", 0, 90_000, 129, "binomial", "probit", "1"),
-    ("p80 logit (odd P16 = 5)", 0, 150_000, 80, "binomial", "logit", "1"),
-    ("p70 poisson + offset + prior (odd P16 = 5, padded stripe)", 2, 100_003, 70, "poisson", "log", "1"),
+    ("p80 logit (odd P16 = 5, forced)", 0, 150_000, 80, "binomial", "logit", "5"),
+    ("p70 poisson + offset + prior (odd P16 = 5, forced, padded stripe)", 2, 100_003, 70, "poisson", "log", "5"),
     ("p232 probit (odd P16 = 15)", 0, 90_001, 232, "binomial", "probit", "1"),
     ("p240 gaussian (odd P16 = 15)", 1, 60_000, 240, "gaussian", "identity", "1"),
-    ("p105 gamma (odd P16 = 7)", 3, 60_000, 105, "gamma", "inverse", "1"),
+    ("p105 gamma (odd P16 = 7, forced)", 3, 60_000, 105, "gamma", "inverse", "7"),
     ("p170 cloglog, few blocks (odd P16 = 11)", 0, 4_000, 170, "binomial", "cloglog", "1"),
     ("p96 cloglog, K1r forced from P16 = 6", 0, 100_000, 96, "binomial", "cloglog", "6"),
     ("p112 poisson + offset + prior, K1r forced from P16 = 6", 2, 80_000, 112, "poisson", "log", "6"),
@@ -135,7 +135,7 @@ def test_mid_width_k1r_and_k1_match_oracle(label, kind, n, p, family, link, thr)
 
 
 @pytest.mark.parametrize("p,name", [(160, "irls_pass_r_kernel<10,binomial,logit>"),
-                                    (80, "irls_pass_r_kernel<5,binomial,logit>")])
+                                    (144, "irls_pass_r_kernel<9,binomial,logit>")])
 def test_shard_reports_k1r(p, name):
     """The bench / roofline label comes from the engine's dispatch (sglm_stats.pass_kernel_name)."""
     with Engine(0) as e:

@@ -1,4 +1,5 @@
-"""Per-kernel gfx950 disassembly of the built device objects (build/obj/{kernels,narrow,wide}.o).
+"""Per-kernel gfx950 disassembly of the built device objects (build/obj/{kernels,fused_odd,narrow,wide}.o;
+ISA_OBJDIR selects a variant build's objects).
 
     python tools/isa_dump.py OUTDIR            # one OUTDIR/<kernel>.s per kernel symbol
     python tools/isa_dump.py --diff DIR_A DIR_B
@@ -19,8 +20,11 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 def dump(outdir: str) -> int:
     os.makedirs(outdir, exist_ok=True)
     count = 0
-    for name in ("kernels", "narrow", "wide"):
-        obj = os.path.join(ROOT, "build", "obj", f"{name}.o")
+    objdir = os.environ.get("ISA_OBJDIR", os.path.join(ROOT, "build", "obj"))  # e.g. build/obj_<variant>
+    for name in ("kernels", "fused_odd", "narrow", "wide"):
+        obj = os.path.join(objdir, f"{name}.o")
+        if not os.path.exists(obj):
+            continue
         with tempfile.TemporaryDirectory() as d:
             fat, co = os.path.join(d, "fatbin"), os.path.join(d, "dev.co")
             subprocess.run([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", obj, os.devnull],

@@ -27,6 +27,12 @@ if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default 
   done
   cat gpurun_out/ab_mid.log
 fi
+if [[ ,$STAGES, == *,sweep,* ]]; then  # mid-width sweep (tools/midp_sweep.py), then the same under rocprofv3
+  timeout -k 10 400 python tools/midp_sweep.py ${SWEEP_P:-} > gpurun_out/midp_sweep.log 2>&1 || { echo "sweep failed"; tail gpurun_out/midp_sweep.log; exit 1; }
+  cat gpurun_out/midp_sweep.log
+  export TMPDIR=/tmp
+  SWEEP_PASSES=3 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_midp" -o midp --output-format csv -- python tools/midp_sweep.py ${SWEEP_P:-} > gpurun_out/prof_midp.log 2>&1 || { echo "sweep prof failed"; tail gpurun_out/prof_midp.log; exit 1; }
+fi
 if [[ ,$STAGES, == *,benchw,* ]]; then  # the other workloads' bench lines (WORKLOADS env: space-separated)
   for w in ${WORKLOADS:-poisson64}; do
     timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-load > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { echo "bench $w failed"; tail -20 gpurun_out/bench_$w.err; exit 1; }

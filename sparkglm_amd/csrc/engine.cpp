@@ -248,7 +248,7 @@ struct sglm_engine : public Backend {
   int64_t proc_scratch_max = 0;  // SGLM_PROC_SCRATCH_MAX (GiB): cap on the procedural chunk scratch (0: none)
   // stats
   int64_t passes = 0, dev_passes = 0;
-  double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
+  double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, last_reduce_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
   bool allow_lm_device = true;  // SGLM_LM_DEVICE=0: LM fits take the two host round trips (tests)
   int64_t lm_device_fits = 0;
@@ -1034,12 +1034,20 @@ struct sglm_engine : public Backend {
     pass_ms += k1;
     reduce_ms += k2;
     last_pass_ms = k1;
+    last_reduce_ms = k2;
     return SGLM_OK;
+  }
+  // An untimed pass (enqueue_pass timed = false: LM.fit on the device, see lm_device) counts the
+  // kernel times of the last timed one.
+  void pass_untimed() {
+    passes += 1;
+    pass_ms += last_pass_ms;
+    reduce_ms += last_reduce_ms;
   }
 
   // H2D beta, the pass kernels and the fixed-order partial reduction into dred -- all
   // asynchronous on this engine's stream (a multi-device handle enqueues every shard first).
-  int enqueue_pass(int mode, const double* beta, double mu0, double ybar, int family, int link) {
+  int enqueue_pass(int mode, const double* beta, double mu0, double ybar, int family, int link, bool timed = true) {
     HIPCHK(hipSetDevice(device));
     if (int rc = check_loaded()) return rc;
     if (beta) {
@@ -1211,15 +1219,17 @@ struct sglm_engine : public Backend {
       // the pass kernel and the reduce record ev0 / ev1 / ev2 as part of their dispatches
       // (hipExtLaunchKernel): separate event records put a ~5 us marker between the kernels,
       // a tenth of an LM.fit on configs[0]
+      hipEvent_t e0 = timed ? ev0 : nullptr, e1 = timed ? ev1 : nullptr, e2 = timed ? ev2 : nullptr;
       if (nblocks > 0) {
-        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, ev0, ev1));
-        else HIPCHK(launch_pass(P16, a, grid, st, ev0, ev1));
+        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, e0, e1));
+        else HIPCHK(launch_pass(P16, a, grid, st, e0, e1));
       } else {
         HIPCHK(hipEventRecord(ev0, st));
         HIPCHK(hipMemsetAsync(dpart, 0, sizeof(double) * stride, st));
         HIPCHK(hipEventRecord(ev1, st));
+        e2 = ev2;
       }
-      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st, ev2));
+      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st, e2));
       return SGLM_OK;
     }
     HIPCHK(hipEventRecord(ev2, st));
@@ -1322,7 +1332,11 @@ struct sglm_engine : public Backend {
     const int64_t plen = packed_len(p);
     if (int rc = ensure_red_len(plen + NS + p)) return rc;
     if (int rc = ensure_small(64)) return rc;
-    if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY)) return rc;
+    // a kernel that carries a completion event ends ~4.5 us later than one that does not (its
+    // end-of-kernel signal; measured on the configs[0] timeline): LM fits time their Gram pass on
+    // every 16th fit and count that time for the others (pass_untimed)
+    const bool timed = (lm_device_fits % 16) == 0;
+    if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, timed)) return rc;
     double* aux = dsmall + NS;  // {ybar, leave-Cholesky flag}
     double* dstat = dred + plen;
     double* dcoef = dred + plen + NS;
@@ -1344,7 +1358,11 @@ struct sglm_engine : public Backend {
     HIPCHK(launch_reduce_stats(dpart, nb, dstat, st));
     HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * (plen + NS + p), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (int rc = pass_timing()) return rc;
+    if (timed) {
+      if (int rc = pass_timing()) return rc;
+    } else {
+      pass_untimed();
+    }
     red_on_device = true;
     std::memcpy(packed, hred, sizeof(double) * plen);
     std::memcpy(s, hred + plen, sizeof(double) * NS);
@@ -2267,7 +2285,7 @@ int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
   h->passes = h->dev_passes = h->lm_device_fits = 0;
-  h->pass_ms = h->reduce_ms = h->last_pass_ms = h->row_ms = h->gram_ms = 0.0;
+  h->pass_ms = h->reduce_ms = h->last_pass_ms = h->last_reduce_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;
   h->load_ms = 0.0;

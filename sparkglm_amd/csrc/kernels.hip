@@ -229,6 +229,8 @@ __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ 
     if (i >= k && row) A[k * LD + i] = lik;
     __syncthreads();
     for (int j0 = k + 1; j0 < p; j0 += U) {  // A(i, j) -= L(i, k) L(j, k), j = k+1 .. i; L(j, k) == 0 skipped
+      // every read of a batch, then the arithmetic, then unconditional stores of the selected values
+      // (no per-element branch and LDS wait: the single wave's step is a serial program)
       double l[U], x[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -239,7 +241,10 @@ __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = j0 + u;
-        if (j < p && i >= j && row && l[u] != 0.0) A[j * LD + i] = x[u] - lik * l[u];
+        if (j < p) {  // wave-uniform
+          const double nv = x[u] - lik * l[u];
+          A[j * LD + i] = (i >= j && row && l[u] != 0.0) ? nv : x[u];
+        }
       }
     }
     __syncthreads();

@@ -519,9 +519,21 @@ struct GeoR {
   using G = Geo<P16>;
   static constexpr int NW = 12, NGW = 8;
   static constexpr int XB = G::XB;                        // doubles per X buffer (K1's image)
-  static constexpr int BETAG_STRIDE = 34;
+  static constexpr int NT = G::NCE / 32;                  // 32-column stripes of the row stage
+  // Row stage of a block: the four row waves, RW = 8 rows each, LPR = 8 lanes per row forming eta
+  // over CPG = 4 columns of every 32-column stripe, the family arithmetic on 8 lanes (K1's lanes and
+  // order at P16 = 16: K1r bitwise K1).  (Measured and not kept, round 4: two row waves of 16 rows
+  // taking alternate blocks -- half the family-arithmetic instructions -- 3-8 % slower at P16 = 9..12,
+  // profiles/r04_midp_ab_run3_rowgroups.txt: the row stage's latency, not its VALU, is what a block
+  // waits for.)  LA: blocks the row stage runs ahead of the Gram.  (Two where the ring has a third
+  // buffer, so its latency would hide under two blocks' MFMAs: measured ±3 % at P16 = 5..12,
+  // profiles/r04_midp_ab_run4_lookahead.txt -- not the bound either; one.)
+  static constexpr int RG = 4;
+  static constexpr int RW = RB / RG, LPR = 64 / RW, CPG = 32 / LPR;
+  static constexpr int BETAG_STRIDE = CPG * NT + 2;       // lane group stride of betag (+2: distinct banks)
   static constexpr int PER_BUF = XB + 4 * RB + 2 * RB + RB;  // X | y, m, offset, prior | w, w*z | eta
-  static constexpr int FIXED = G::NCE + NW * NS + 8 * BETAG_STRIDE + 2 + 6;
+  static constexpr int NCNT = 10;                         // counters: flag | ready[4] | done[4] (uint32)
+  static constexpr int FIXED = G::NCE + NW * NS + LPR * BETAG_STRIDE + NCNT / 2 + 6;
   static constexpr int LDS_MAX = 160 * 1024 / 8;
   static constexpr int NBUF = 4 * PER_BUF + FIXED <= LDS_MAX ? 4 : (3 * PER_BUF + FIXED <= LDS_MAX ? 3 : 2);
   static constexpr int OFF_X = 0;                         // [NBUF][XB]
@@ -531,16 +543,16 @@ struct GeoR {
   static constexpr int OFF_BETA = OFF_ETA + NBUF * RB;    // [NCE]
   static constexpr int OFF_RED = OFF_BETA + G::NCE;       // [NW][NS]
   // [8 lane groups][4 NCE/32 (+2 pad: the groups' ds_read_b128 broadcasts land in distinct banks)]
-  static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas
-  static constexpr int OFF_FLAG = OFF_BETAG + 8 * BETAG_STRIDE;        // counters: row-wave staging, ready, done (uint32)
-  static constexpr int OFF_INIT = OFF_FLAG + 2;                         // [6] init_const
+  static constexpr int OFF_BETAG = OFF_RED + NW * NS;     // row_stage_r's betas [LPR groups][BETAG_STRIDE]
+  static constexpr int OFF_FLAG = OFF_BETAG + LPR * BETAG_STRIDE;      // counters (uint32)
+  static constexpr int OFF_INIT = OFF_FLAG + NCNT / 2;                  // [6] init_const
   static constexpr int LDS_DOUBLES = OFF_INIT + 6;
   static_assert(LDS_DOUBLES == NBUF * PER_BUF + FIXED, "layout");
+  static constexpr int LA = 1;
+  static_assert(LA >= 1 && LA < NBUF, "row-stage lookahead within the ring");
   static_assert(XB % 2 == 0 && OFF_V % 2 == 0, "LDS-DMA destinations 16-byte aligned");
   static constexpr int QPW = P16;                         // column quads each row wave stages
-  static constexpr int NT = G::NCE / 32;                  // 32-column stripes of the row stage
   static_assert(LDS_DOUBLES * 8 <= 160 * 1024, "LDS");
-  static_assert(4 * NT <= BETAG_STRIDE, "32-column stripes of the row stage");
   // every Gram wave's tiles fit NSEG segments and the eight runs cover the triangle
   static constexpr bool tiles_ok() {
     return TilesR<P16, 0>::NT + TilesR<P16, 1>::NT + TilesR<P16, 2>::NT + TilesR<P16, 3>::NT + TilesR<P16, 4>::NT +
@@ -632,9 +644,9 @@ template <int P16, int FAM, int LNK>
 __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs& a, int64_t blk, int rw, int lane,
                                             double& s_dev, double& s_aux) {
   using G = Geo<P16>;
-  constexpr int RW = 8, CPG = 4, NT = GeoR<P16>::NT;
-  static_assert(P16 != 16 || (G::RW == RW && G::CPG == CPG && NT == 8), "K1's P16 = 16 row-stage geometry");
   using R = GeoR<P16>;
+  constexpr int RW = R::RW, CPG = R::CPG, NT = R::NT;
+  static_assert(P16 != 16 || (G::RW == RW && G::CPG == CPG && NT == 8), "K1's P16 = 16 row-stage geometry");
   const double* xs = lds + R::OFF_X + buf * R::XB;
   const int rl = lane % RW, g = lane / RW;
   const double* bg = lds + R::OFF_BETAG + g * R::BETAG_STRIDE;
@@ -648,7 +660,7 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
   if (a.mode == MODE_IRLS) {
     double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < CPG / 2; ++h) {
       double xv[2][NT], bv[2][NT];
 #pragma unroll
       for (int uu = 0; uu < 2; ++uu) {
@@ -669,7 +681,7 @@ __device__ __forceinline__ void row_stage_r(double* lds, int buf, const PassArgs
       __builtin_amdgcn_sched_group_barrier(0x002, 2 * NT, 2);
     }
     eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
-    eta = add_xor8(eta);
+    if constexpr (RW <= 8) eta = add_xor8(eta);
     eta = add_xor16(eta);
     eta = add_xor32(eta);
   }
@@ -775,18 +787,26 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
     if (later >= 1) return wait_vmcnt<PER>();
     wait_vmcnt<0>();
   };
-  // No block barrier: three LDS counters order the ring of NBUF buffers.
-  //   flag : +1 per row wave when its LDS-DMA part of a block has landed (4 per block)
-  //   ready: +1 per row wave when its rows of a block's row stage are in the w buffer (4 per block)
-  //   done : +1 per wave when it has finished reading a block: the Gram waves' MFMAs, the row
-  //          waves' X'Wz (12 per block)
-  // A Gram wave starts block b once ready(b) and may run up to one block ahead of the slowest
-  // Gram wave, so the two Gram waves of a SIMD no longer end every block with one of them alone
-  // on the MFMA pipe; the row waves stage block b+NBUF into block b's buffers after done(b).
-  // (The row stage of b+NBUF rewrites w(b): it follows that row wave's own wait for done(b), and its
-  // flag round orders it after every row wave's DMA of b+NBUF.)
-  unsigned* ready = flag + 1;
-  unsigned* done = flag + 2;
+  // No block barrier: LDS counters order the ring of NBUF buffers.
+  //   flag      : +1 per row wave when its LDS-DMA part of a block has landed (4 per block); every row
+  //               wave bumps it once per block and then waits for all four, so it acts as a barrier
+  //               among the row waves and a plain count is exact
+  //   ready[s]  : +1 per row-stage wave when its rows of the block in ring slot s are in the w buffer
+  //               (RG per block)
+  //   done[s]   : +1 per wave when it has finished reading the block in slot s: the Gram waves' MFMAs,
+  //               the row waves' X'Wz (12 per block)
+  // Per-slot counters: the Gram waves are not coupled to each other, and a fast one may finish a block
+  // while a slow one is still in an earlier block -- one counter for all blocks would then count the
+  // fast wave's later block as the slow wave's, and the slot could be restaged under the slow wave.
+  // A slot's next use cannot begin before its counters reached the current round's targets (its DMA
+  // waits for done[s]), so a per-slot count is exact.
+  // A Gram wave starts block b once ready(b), so the two Gram waves of a SIMD no longer end every
+  // block with one of them alone on the MFMA pipe; the row waves stage block b+NBUF into block b's
+  // slot after done(b).  (The row stage of b+NBUF rewrites w(b): it follows the flag round of
+  // b+NBUF, i.e. every row wave's DMA of b+NBUF, each issued after done(b).)
+  unsigned* ready = flag + 1;     // [NB]
+  unsigned* done = flag + 1 + 4;  // [NB]
+  constexpr int RG = R::RG, LA = R::LA;
   auto spin = [&](unsigned* c, unsigned target) {
     while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
   };
@@ -795,43 +815,55 @@ __device__ __forceinline__ void pass_body_r(double* lds, const PassArgs& a, int 
   };
   auto next_buf = [](int b) { return b + 1 == NB ? 0 : b + 1; };
   if constexpr (row_wave) {
-    if (b0 < b1) {
-      wait_landed(std::min<int64_t>(b1 - b0 - 1, NB - 1));
-      bump(flag);
-      spin(flag, 4u);
-      row_stage_r<P16, FAM, LNK>(lds, 0, a, b0, si, lane, s_dev, s_aux);
-      bump(ready);
+    // row stages of the first LA blocks (slots 0 .. LA-1), each after its flag round
+#pragma unroll
+    for (int c = 0; c < LA; ++c) {
+      if (b0 + c < b1) {
+        wait_landed(std::min<int64_t>(b1 - b0 - 1, NB - 1) - c);
+        bump(flag);
+        spin(flag, 4u * (c + 1));
+        row_stage_r<P16, FAM, LNK>(lds, c, a, b0 + c, si, lane, s_dev, s_aux);
+        bump(ready + c);
+      }
     }
     int cur = 0;
+    unsigned rnd = 0;  // uses of slot cur before block blk
 #pragma unroll 1
-    for (int64_t blk = b0; blk < b1; ++blk, cur = next_buf(cur)) {
-      if (blk + 1 < b1) {
-        wait_landed(std::min<int64_t>(b1 - blk - 2, NB - 2));
+    for (int64_t blk = b0; blk < b1; ++blk) {
+      if (blk + LA < b1) {  // the row stage of block blk + LA
+        wait_landed(std::min<int64_t>(b1 - 1, blk + NB - 1) - (blk + LA));
         bump(flag);
-        spin(flag, (unsigned)(4 * (blk + 2 - b0)));
-        row_stage_r<P16, FAM, LNK>(lds, next_buf(cur), a, blk + 1, si, lane, s_dev, s_aux);
-        bump(ready);
+        spin(flag, (unsigned)(4 * (blk + LA - b0 + 1)));
+        int sl = cur + LA;
+        if (sl >= NB) sl -= NB;
+        row_stage_r<P16, FAM, LNK>(lds, sl, a, blk + LA, si, lane, s_dev, s_aux);
+        bump(ready + sl);
       }
-      // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them
-      // (each row wave bumps flag after its row stage of blk); the last block has no such round
-      if (blk + 1 >= b1) spin(ready, (unsigned)(4 * (blk - b0 + 1)));
+      // X'Wz of block blk reads every row wave's w*z of it: the flag round above ordered them (each
+      // row wave bumps flag after its row stage of blk); the last LA blocks have no such round
+      if (blk + LA >= b1) spin(ready + cur, (unsigned)(RG * (rnd + 1)));
       if (do_gram) xz_rows_r<P16, si>(lds, cur, lane, xz);
-      bump(done);  // this row wave's reads of block blk (X'Wz) are complete
+      bump(done + cur);  // this row wave's reads of block blk (X'Wz) are complete
       if (blk + NB < b1) {
-        spin(done, (unsigned)(12 * (blk - b0 + 1)));
+        spin(done + cur, 12u * (rnd + 1));
         stage_block_r<P16>(lds, cur, a, blk + NB, si, voff, vvoff);
       }
+      cur = next_buf(cur);
+      if (cur == 0) ++rnd;
     }
   } else {
     int cur = 0;
+    unsigned rnd = 0;
 #pragma unroll 1
-    for (int64_t blk = b0; blk < b1; ++blk, cur = next_buf(cur)) {
-      spin(ready, (unsigned)(4 * (blk - b0 + 1)));
+    for (int64_t blk = b0; blk < b1; ++blk) {
+      spin(ready + cur, (unsigned)(RG * (rnd + 1)));
       if (do_gram) gram_steps_r<P16, WV>(lds, cur, lane, acc);
       if constexpr (WV == 0)  // the row stage's eta of this block (IRLS passes that keep it)
         if (a.eta_out && a.mode == MODE_IRLS && lane < RB && blk * RB + lane < a.n)
           a.eta_out[blk * RB + lane] = lds[R::OFF_ETA + cur * RB + lane];
-      bump(done);
+      bump(done + cur);
+      cur = next_buf(cur);
+      if (cur == 0) ++rnd;
     }
   }
   if (row_wave) __builtin_amdgcn_s_setprio(0);
@@ -890,10 +922,10 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
   for (int c = threadIdx.x; c < G::NCE; c += 64 * R::NW) {
     const double b = (a.beta && c < a.p) ? a.beta[c] : 0.0;
     lds[R::OFF_BETA + c] = b;
-    // betag[g][t * 4 + u] = beta[4 g + u + 32 t] (row_stage_r)
-    lds[R::OFF_BETAG + ((c & 31) >> 2) * R::BETAG_STRIDE + (c >> 5) * 4 + (c & 3)] = b;
+    // betag[g][t * CPG + u] = beta[CPG g + u + 32 t] (row_stage_r)
+    lds[R::OFF_BETAG + ((c & 31) / R::CPG) * R::BETAG_STRIDE + (c >> 5) * R::CPG + (c & 31) % R::CPG] = b;
   }
-  if (threadIdx.x < 3) ((unsigned*)(lds + R::OFF_FLAG))[threadIdx.x] = 0u;
+  if (threadIdx.x < R::NCNT) ((unsigned*)(lds + R::OFF_FLAG))[threadIdx.x] = 0u;
   if constexpr (G::NCE > G::NC) {  // odd P16: the row stage's last stripe reads 16 columns no DMA writes
     for (int e = threadIdx.x; e < (G::NCE - G::NC) * RB; e += 64 * R::NW) {
       const int c = G::NC + e / RB, r = e % RB;

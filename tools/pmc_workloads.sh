@@ -16,6 +16,8 @@ for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
     logit512) run_wl logit512 8000000 512 0 binomial logit 0 SGLM_WIDE_OVERLAP=2 ;;
     gamma2048) run_wl gamma2048 2000000 2048 3 gamma inverse 0 SGLM_WIDE_OVERLAP=3 ;;
     logit32) run_wl logit32 100000000 32 0 binomial logit ;;   # logit1b's per-row pattern
+    mid160) run_wl mid160 10000000 160 0 binomial logit ;;     # mid-width K1r<10>
+    mid96) run_wl mid96 15000000 96 0 binomial logit ;;        # mid-width K1<6>, three workgroups per CU
     logit512p) run_wl logit512p 8000000 512 0 binomial logit 1 ;;  # procedural shard (HBM-scratch chunks)
   esac
 done

@@ -87,6 +87,11 @@ MID = [
     ("p105 gamma (odd P16 = 7, forced)", 3, 60_000, 105, "gamma", "inverse", "7"),
     ("p170 cloglog, few blocks (odd P16 = 11)", 0, 4_000, 170, "binomial", "cloglog", "1"),
     ("p96 cloglog, K1r forced from P16 = 6", 0, 100_000, 96, "binomial", "cloglog", "6"),
+    # the ring of up to four row-block buffers (GeoR::NBUF = 4 at P16 <= 8, 3 up to 12) partly filled:
+    # fewer blocks than workgroups, and three blocks per workgroup
+    ("p96 logit, fewer blocks than workgroups, 4-deep ring", 0, 5_000, 96, "binomial", "logit", "6"),
+    ("p120 poisson + offset + prior, three blocks per workgroup, 4-deep ring", 2, 24_576, 120, "poisson", "log", "7"),
+    ("p176 probit, two blocks per workgroup, 3-deep ring", 0, 16_384, 176, "binomial", "probit", "1"),
     ("p112 poisson + offset + prior, K1r forced from P16 = 6", 2, 80_000, 112, "poisson", "log", "6"),
 ]
 

@@ -512,8 +512,10 @@ struct TilesR {
 
 // K1r's LDS: a ring of NBUF row-block buffers -- as deep as 160 KB allows (4 up to P16 = 8, 3 up to
 // 12, 2 above): the DMA of block b + NBUF is issued when block b is consumed, so a row wave finds the
-// next block landed instead of waiting out its HBM latency (with two buffers that latency plus the
-// row stage was the per-block critical path whenever the Gram of a block is short, i.e. below P16 ~ 10).
+// next block landed instead of waiting out its HBM latency.  (With two buffers that wait sat on the
+// row waves' per-block path; the deeper ring measured +1-9 % at P16 = 9..12 and +-0 at 16,
+// profiles/r04_midp_ab_run2_ring.txt -- at the mid widths the clock and the row stage's VALU bound
+// the pass more than the DMA latency did)
 template <int P16>
 struct GeoR {
   using G = Geo<P16>;

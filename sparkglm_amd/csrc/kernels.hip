@@ -188,81 +188,95 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // LM.fit's p x p solve on the device (engine.cpp lm_device; p <= 64): the host solver's Cholesky
 // (solve.cpp chol_factor + chol_solve), element for element in the same operation order without
 // contraction, so the coefficients come out bitwise the host's (driver.cpp lm_drive checks that and
-// otherwise reruns the residual pass at its own).  Lane i owns row i.  The factorization runs
-// right-looking: step k takes column k's pivot, scales it, then subtracts L(i,k) L(j,k) from every
-// trailing element (i, j) -- each element still receives its subtractions in ascending k, exactly
-// chol_factor's left-looking order, but the subtractions of one step are independent (no dependent
-// chain of length j per column, which made the first, left-looking form 40K cycles at p = 20).
-// Both triangular solves are column sweeps: the pivot's quotient on its lane, handed to the others
-// by readlane.  Out: beta[p]; aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where the host
-// would leave Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO:
-// solve.cpp chol_pivot_ratio).
+// otherwise reruns the residual pass at its own).  Four waves; in every wave lane i is row i.
+// The factorization runs right-looking: step k takes column k's pivot and scales the column, then
+// subtracts L(i,k) L(j,k) from every trailing element (i, j) -- each element still receives its
+// subtractions in ascending k, exactly chol_factor's left-looking order, but one step's subtractions
+// are independent: waves 0-2 split the trailing columns (j mod 3), each forming the pivot and L(:,k)
+// itself (the same operations, so the same values) and taking L(j,k) from its own lanes by readlane;
+// wave 3 runs the forward sweep L t = b one column behind.  One barrier per step.  The back
+// substitution is a column sweep on one wave (the host chol_solve's order).  The first forms -- one
+// wave, left-looking, one LDS read and branch per subtraction -- took 37 us at p = 20; one wave
+// right-looking 26 us (the chain of 20 pivots at single-wave latency plus all the updates).
+// Out: beta[p]; aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where the host would leave
+// Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO: solve.cpp chol_pivot_ratio).
 __device__ __forceinline__ double lane_bcast(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
-__global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
-                                                     double* __restrict__ beta, double* __restrict__ aux) {
+__global__ void __launch_bounds__(256) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
+                                                      double* __restrict__ beta, double* __restrict__ aux) {
 #pragma clang fp contract(off)
-  constexpr int LD = 65, U = 8;  // A(r, c) at A[c LD + r]: column reads by lane conflict-free, row reads 2-way
-  __shared__ double A[64 * LD], dg[64];
-  const int i = threadIdx.x;
+  constexpr int LD = 65, U = 8, NUPD = 3;  // A(r, c) at A[c LD + r]; waves 0..NUPD-1 update, wave NUPD solves
+  __shared__ double A[64 * LD], dg[64], tsh[64];
+  __shared__ int fail_sh;
+  const int i = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool row = i < p;
   const int64_t tri = (int64_t)p * (p + 1) / 2;
-  for (int e = i; e < p * p; e += 64) {  // unpack_gram: A(r, c) = packed[max(r, c) (max + 1) / 2 + min(r, c)]
+  for (int e = threadIdx.x; e < p * p; e += 256) {  // unpack_gram: A(r, c) = packed[max(r, c) (max + 1) / 2 + min(r, c)]
     const int r = e % p, c = e / p, hi = r > c ? r : c, lo = r > c ? c : r;
     A[c * LD + r] = packed[hi * (hi + 1) / 2 + lo];
   }
-  if (row) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
-  double ti = row ? packed[tri + i] : 0.0;
+  if (threadIdx.x < 64 && row) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
+  if (threadIdx.x == 0) fail_sh = 0;
+  double ti = row ? packed[tri + i] : 0.0;  // wave NUPD: the forward sweep's t
   __syncthreads();
-  int fail = 0;
   for (int k = 0; k < p; ++k) {  // chol_factor
     const double d = A[k * LD + k];
     const double aik = A[k * LD + i];
-    if (!(d > 0.0) || !isfinite(d)) {
-      fail = 1;
+    if (!(d > 0.0) || !isfinite(d)) {  // every wave sees the same d: a uniform exit
+      if (threadIdx.x == 0) fail_sh = 1;
       break;
     }
     const double sq = sqrt(d);
     const double inv = 1.0 / sq;
     const double lik = (i == k) ? sq : aik * inv;  // L(i, k), lanes i >= k
-    if (i >= k && row) A[k * LD + i] = lik;
-    __syncthreads();
-    for (int j0 = k + 1; j0 < p; j0 += U) {  // A(i, j) -= L(i, k) L(j, k), j = k+1 .. i; L(j, k) == 0 skipped
-      // every read of a batch, then the arithmetic, then unconditional stores of the selected values
-      // (no per-element branch and LDS wait: the single wave's step is a serial program)
-      double l[U], x[U];
+    if (wv < NUPD) {
+      // A(i, j) -= L(i, k) L(j, k) for this wave's trailing columns j = k+1+wv, k+1+wv+NUPD, ...; L(j, k) == 0 skipped
+      for (int j0 = k + 1 + wv; j0 < p; j0 += NUPD * U) {
+        double l[U], x[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 + u < p ? j0 + u : p - 1;
-        l[u] = A[k * LD + j];
-        x[u] = A[j * LD + i];
-      }
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + NUPD * u < p ? j0 + NUPD * u : p - 1;
+          l[u] = lane_bcast(lik, j);
+          x[u] = A[j * LD + i];
+        }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 + u;
-        if (j < p) {  // wave-uniform
-          const double nv = x[u] - lik * l[u];
-          A[j * LD + i] = (i >= j && row && l[u] != 0.0) ? nv : x[u];
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + NUPD * u;
+          if (j < p) {  // wave-uniform
+            const double nv = x[u] - lik * l[u];
+            A[j * LD + i] = (i >= j && row && l[u] != 0.0) ? nv : x[u];
+          }
         }
       }
+    } else {
+      // L t = b, column k: t_k /= L(k, k); t_i -= L(i, k) t_k, i > k
+      const double tk = lane_bcast(ti / sq, k);
+      if (i == k) ti = tk;
+      if (i > k && row) ti -= lik * tk;
     }
     __syncthreads();
+    // column k of L into A after every wave has read A(k, k) and A(:, k) (only the solves and the
+    // pivot ratio read it again; the next step reads column k + 1)
+    if (wv == 0 && i >= k && row) A[k * LD + i] = lik;
   }
+  __syncthreads();
+  const int fail = fail_sh;
   if (!fail) {
-    for (int j = 0; j < p; ++j) {  // L t = b: t_j /= L(j, j); t_i -= L(i, j) t_j, i > j
-      const double tj = lane_bcast(ti / A[i * LD + i], j);
-      if (i == j) ti = tj;
-      if (i > j && row) ti -= A[j * LD + i] * tj;
+    if (wv == NUPD) tsh[i] = ti;
+    __syncthreads();
+    if (wv == 0) {
+      double tb = tsh[i];
+      for (int r = p - 1; r >= 0; --r) {  // L' x = t: x_r = t_r / L(r, r); t_i -= L(r, i) x_r, i < r
+        const double xr = lane_bcast(tb / A[i * LD + i], r);
+        if (i == r) tb = xr;
+        if (i < r) tb -= A[i * LD + r] * xr;
+      }
+      if (row) beta[i] = tb;
     }
-    for (int r = p - 1; r >= 0; --r) {  // L' x = t: x_r = t_r / L(r, r); t_i -= L(r, i) x_r, i < r
-      const double xr = lane_bcast(ti / A[i * LD + i], r);
-      if (i == r) ti = xr;
-      if (i < r) ti -= A[i * LD + r] * xr;
-    }
-    if (row) beta[i] = ti;
   }
-  if (i == 0) {
+  if (threadIdx.x == 0) {
     double r = 1.0;  // chol_pivot_ratio
     if (!fail)
       for (int j = 0; j < p; ++j) {
@@ -434,7 +448,7 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hip
 
 hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st) {
   if (p < 1 || p > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lm_chol_kernel, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux);
+  hipLaunchKernelGGL(lm_chol_kernel, dim3(1), dim3(256), 0, st, packed, p, ratio_min, beta, aux);
   return hipGetLastError();
 }
 

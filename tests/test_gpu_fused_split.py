@@ -1,4 +1,4 @@
-"""The split-role fused pass K1r (kernels.hip irls_pass_r_kernel: two MFMA-only "Gram waves" and
+"""The split-role fused pass K1r (fused.hpp irls_pass_r_kernel: two MFMA-only "Gram waves" and
 one "row wave" per SIMD) against K1 (irls_pass_kernel, SGLM_FUSED_SPLIT=0, read when an engine is
 created).
 

@@ -87,6 +87,7 @@ MID = [
     ("p105 gamma (odd P16 = 7, forced)", 3, 60_000, 105, "gamma", "inverse", "7"),
     ("p170 cloglog, few blocks (odd P16 = 11)", 0, 4_000, 170, "binomial", "cloglog", "1"),
     ("p96 cloglog, K1r forced from P16 = 6", 0, 100_000, 96, "binomial", "cloglog", "6"),
+    ("p128 logit, K1r forced from P16 = 8", 0, 80_000, 128, "binomial", "logit", "8"),
     # the ring of up to four row-block buffers (GeoR::NBUF = 4 at P16 <= 8, 3 up to 12) partly filled:
     # fewer blocks than workgroups, and three blocks per workgroup
     ("p96 logit, fewer blocks than workgroups, 4-deep ring", 0, 5_000, 96, "binomial", "logit", "6"),

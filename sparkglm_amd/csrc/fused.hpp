@@ -91,6 +91,106 @@ struct Geo {
   static constexpr int ntiles(int wv) { return lo_row(wv) + hi_row(wv) + 2; }
 };
 
+template <int P16>
+struct TileSeq {
+  static constexpr int T = P16 * (P16 + 1) / 2;
+  static constexpr int seq_row(int i) { return (i & 1) ? P16 - 1 - (i >> 1) : (i >> 1); }  // i-th row of the sequence
+  static constexpr int seq_start(int i) {  // first sequence index of row seq_row(i)
+    int t = 0;
+    for (int k = 0; k < i; ++k) t += seq_row(k) + 1;
+    return t;
+  }
+  static constexpr int seq_of(int t) {  // sequence row holding sequence tile t
+    int i = 0;
+    while (i + 1 < P16 && seq_start(i + 1) <= t) ++i;
+    return i;
+  }
+};
+constexpr int NSEG = 4;
+
+// Tiles [TLO, THI) of the paired-row tile sequence as up to NSEG segments, each a run of tiles
+// (row, j0 .. j0 + cnt - 1) of one block row (one A operand per segment, B = column block j).
+// diag(s): the segment holds its row's diagonal tile (row, row), the sequence's last tile of that
+// row -- that segment forms the row block's X'Wz, so every block row's X'Wz is formed exactly once.
+template <int P16, int TLO, int THI>
+struct TileRun {
+  using S = TileSeq<P16>;
+  static constexpr int row(int s) {
+    if (THI <= TLO) return -1;
+    const int i = S::seq_of(TLO) + s;
+    return i <= S::seq_of(THI - 1) ? S::seq_row(i) : -1;
+  }
+  static constexpr int j0(int s) { return s == 0 && THI > TLO ? TLO - S::seq_start(S::seq_of(TLO)) : 0; }
+  static constexpr int cnt(int s) {
+    if (row(s) < 0) return 0;
+    const int i = S::seq_of(TLO) + s;
+    const int b = i == S::seq_of(TLO) ? TLO : S::seq_start(i);  // first sequence tile in the run
+    const int e = S::seq_start(i) + S::seq_row(i) + 1;          // end of the row in the sequence
+    return (e < THI ? e : THI) - b;
+  }
+  static constexpr bool diag(int s) { return cnt(s) > 0 && j0(s) + cnt(s) - 1 == row(s); }
+  static constexpr int off(int s) {
+    int o = 0;
+    for (int k = 0; k < s; ++k) o += cnt(k);
+    return o;
+  }
+  static constexpr int NT = off(NSEG);
+  static constexpr int seg_of(int k) {
+    int sg = 0;
+    while (sg + 1 < NSEG && off(sg + 1) <= k) ++sg;
+    return sg;
+  }
+  static_assert(NT == (THI > TLO ? THI - TLO : 0), "the run fits NSEG segments");
+};
+
+// K1's tiles.  P16 = 16: wave WV owns block rows LO = lo_row(WV) and HI = hi_row(WV) whole -- two
+// segments (the row waves' rows chosen short; K1r is bitwise this).  Other P16: the tile sequence
+// cut into NW contiguous runs, the row waves' runs ROW_TILES shorter than the MFMA-only waves'.
+// The row stage of the next block runs on the row waves between their k-steps and the block ends
+// at a barrier; with whole row pairs the waves' shares were fixed by the pairs (P16 = 6: 8 / 6 / 7
+// tiles, the single row wave's row stage on top of its 6) -- PMC, K1<6>: 39 % of wave cycles parked,
+// profiles/r04_stalls/mid96.json.  Same-box A/B (profiles/r04_midp_ab_run6_k1runs.txt): P16 = 6
+// with one row wave runs best 3 tiles short (8 / 5 / 8: p = 80 10.59 (round 3) -> 9.18 ms, p = 96
+// 9.15 -> 8.02 ms; 0 or 5 short: 9.4-10.0 / 8.3-8.6), P16 = 8 with two row waves best evenly
+// (9 tiles each: p = 112 10.16 -> 9.76 ms; 3 short 10.28).  Runs only move which wave forms a
+// tile; every tile and X'Wz column sums the same k-steps in the same order.
+template <int P16>
+struct K1Runs {
+  using G = Geo<P16>;
+  static constexpr int ROW_TILES = G::NRW == 1 ? 3 : 0;
+  static constexpr bool is_row(int w) { return w >= G::ROW0 && w < G::ROW0 + G::NRW; }
+  static constexpr int LR = G::NA > 0 ? ((G::T - G::NA * ROW_TILES) / G::NW > 1 ? (G::T - G::NA * ROW_TILES) / G::NW : 1)
+                                      : G::T;  // tiles of a row wave
+  static constexpr int len(int w) {
+    if (G::NA == 0) return G::T;
+    if (is_row(w)) return LR;
+    const int rest = G::T - G::NRW * LR;
+    int ia = 0;  // issuer index of wave w
+    for (int v = 0; v < w; ++v)
+      if (!is_row(v)) ++ia;
+    return rest * (ia + 1) / G::NA - rest * ia / G::NA;
+  }
+  static constexpr int lo(int w) {
+    int t = 0;
+    for (int v = 0; v < w; ++v) t += len(v);
+    return t;
+  }
+  static_assert(lo(G::NW) == G::T, "the runs cover the tile triangle");
+};
+template <int P16, int WV, bool RUNS = (P16 != 16)>
+struct TilesK1 : TileRun<P16, K1Runs<P16>::lo(WV), K1Runs<P16>::lo(WV + 1)> {};
+template <int P16, int WV>
+struct TilesK1<P16, WV, false> {
+  static constexpr int LO = Geo<P16>::lo_row(WV), HI = Geo<P16>::hi_row(WV);
+  static constexpr int row(int s) { return s == 0 ? LO : (s == 1 ? HI : -1); }
+  static constexpr int j0(int) { return 0; }
+  static constexpr int cnt(int s) { return s == 0 ? LO + 1 : (s == 1 ? HI + 1 : 0); }
+  static constexpr bool diag(int s) { return s < 2; }
+  static constexpr int off(int s) { return s == 0 ? 0 : (s == 1 ? LO + 1 : LO + HI + 2); }
+  static constexpr int NT = LO + HI + 2;
+  static constexpr int seg_of(int k) { return k <= LO ? 0 : 1; }
+};
+
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left open (gfx9 encoding).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -224,19 +324,19 @@ __device__ __forceinline__ void row_stage(double* lds, int buf, int wb, const Pa
   }
 }
 
-// MFMA k-steps [S0, S1) of one block for wave WV (compile-time, so every operand is a
-// static LDS offset).  Wave WV owns block rows LO = lo_row(WV) and HI = P16-1-WV of the lower
-// tile grid: tiles (LO, 0..LO) then (HI, 0..HI).  Lane l reads X[k0 + (l>>4)][16b + (l&15)];
-// the A operand (blocks LO / HI) is scaled by the lane's row weight, the B operands are
-// used straight from LDS.  X'Wz accumulates on the VALU from the same A fragments.
-// A phase is RB/8 k-steps starting at S0.  Narrow variants (P16 <= 8: at most 9 MFMAs per
-// k-step) unroll the phase so the next k-step's LDS operand reads issue under the current
-// k-step's MFMAs; wide variants carry enough MFMAs per k-step to cover the read latency.
+// MFMA k-steps [S0, S0 + NST) of one block for wave WV (compile-time, so every operand is a
+// static LDS offset): the wave's tiles (TilesK1 segments; P16 = 16: block rows LO, HI whole).  Lane l
+// reads X[k0 + (l>>4)][16b + (l&15)]; the A operand (a segment's block row) is scaled by the lane's
+// row weight, the B operands are used straight from LDS.  X'Wz accumulates on the VALU from the A
+// fragments of the segments that hold their row's diagonal tile.  A phase is RB/8 k-steps starting
+// at S0.  Narrow variants (P16 <= 8: at most 9 MFMAs per k-step) unroll the phase so the next
+// k-step's LDS operand reads issue under the current k-step's MFMAs; wide variants carry enough
+// MFMAs per k-step to cover the read latency.
 template <int P16, int WV, int NST = RB / 8>
 __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, int lane, int S0,
-                                           d4 (&acc)[Geo<P16>::ntiles(WV)], double& xz_lo, double& xz_hi) {
+                                           d4 (&acc)[TilesK1<P16, WV>::NT], double (&xz)[NSEG]) {
   using G = Geo<P16>;
-  constexpr int LO = Geo<P16>::lo_row(WV), HI = Geo<P16>::hi_row(WV);
+  using T = TilesK1<P16, WV>;
   constexpr int UNR = P16 <= 8 ? NST : 1;
   const double* xs = lds + G::OFF_X + buf * G::XB;
   const double* w = lds + G::OFF_W + wb * 2 * RB;
@@ -247,16 +347,23 @@ __device__ __forceinline__ void gram_steps(const double* lds, int buf, int wb, i
     const int r = 4 * (S0 + j) + rq;
     const double* base = colbase + (r ^ (2 * cl));
     const double wr = w[r], wzr = w[RB + r];
-    const double x_lo = base[G::BSTR * LO], x_hi = base[G::BSTR * HI];
-    const double a_lo = x_lo * wr, a_hi = x_hi * wr;
-    xz_lo += x_lo * wzr;
-    xz_hi += x_hi * wzr;
+    double av[NSEG];
 #pragma unroll
-    for (int k = 0; k < Geo<P16>::ntiles(WV); ++k) {
-      constexpr int dummy = 0;
-      (void)dummy;
-      const double b = base[G::BSTR * (k <= LO ? k : k - LO - 1)];
-      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(k <= LO ? a_lo : a_hi, b, acc[k], 0, 0, 0);
+    for (int sg = 0; sg < NSEG; ++sg) {
+      av[sg] = 0.0;
+      if constexpr (true) {
+        if (T::cnt(sg) > 0) {
+          const double x = base[G::BSTR * (T::row(sg) >= 0 ? T::row(sg) : 0)];
+          av[sg] = x * wr;
+          if (T::diag(sg)) xz[sg] += x * wzr;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < T::NT; ++k) {
+      const int sg = T::seg_of(k);
+      const double b = base[G::BSTR * (T::j0(sg) + k - T::off(sg))];
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sg], b, acc[k], 0, 0, 0);
     }
   }
 }
@@ -289,10 +396,11 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
   constexpr int KA = P16 == 16 ? 0 : 2;
   unsigned* flag = (unsigned*)(lds + G::OFF_FLAG);
 
-  d4 acc[G::ntiles(WV)];
+  using TK = TilesK1<P16, WV>;
+  d4 acc[TK::NT];
 #pragma unroll
-  for (int k = 0; k < G::ntiles(WV); ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
-  double xz_lo = 0.0, xz_hi = 0.0, s_dev = 0.0, s_aux = 0.0;
+  for (int k = 0; k < TK::NT; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+  double xz[NSEG] = {0.0, 0.0, 0.0, 0.0}, s_dev = 0.0, s_aux = 0.0;
 
   if (issuer && b0 < b1) {
     stage_block<P16>(lds, 0, a, b0, si, lane);
@@ -310,32 +418,32 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
     if constexpr (G::NA > 0) {
       if constexpr (!row_wave) {
         // MFMA-only wave: after KA k-steps, publish that its part of block blk+1 has landed
-        if (has_gram) gram_steps<P16, WV, KA>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+        if (has_gram) gram_steps<P16, WV, KA>(lds, cur & 1, cur & 1, lane, 0, acc, xz);
         if (has_next) {
           wait_vmcnt<0>();
           if (lane == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (has_gram) gram_steps<P16, WV, RB / 4 - KA>(lds, cur & 1, cur & 1, lane, KA, acc, xz_lo, xz_hi);
+        if (has_gram) gram_steps<P16, WV, RB / 4 - KA>(lds, cur & 1, cur & 1, lane, KA, acc, xz);
       } else {
         // row wave: after K1 k-steps, wait until every issuer's part of block blk+1 landed
-        if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+        if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz);
         if (has_next) {
           const unsigned target = (unsigned)(G::NA * (blk + 2 - b0));
           while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
             __builtin_amdgcn_s_sleep(1);
           row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
         }
-        if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
+        if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz);
       }
     } else {
       // single wave: it stages, waits and computes everything itself
-      if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz_lo, xz_hi);
+      if (has_gram) gram_steps<P16, WV, K1>(lds, cur & 1, cur & 1, lane, 0, acc, xz);
       if (has_next) {
         if (blk + 1 == b0 && b0 + 1 < b1) wait_vmcnt<G::QMAX + G::VMAX>();
         else wait_vmcnt<0>();
         row_stage<P16, FAM, LNK>(lds, cur ^ 1, cur ^ 1, a, blk + 1, wv, lane, s_dev, s_aux);
       }
-      if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz_lo, xz_hi);
+      if (has_gram) gram_steps<P16, WV, RB / 4 - K1>(lds, cur & 1, cur & 1, lane, K1, acc, xz);
     }
     lds_barrier();
     if (issuer && blk >= b0 && blk + 2 < b1) stage_block<P16>(lds, cur, a, blk + 2, si, lane);
@@ -347,21 +455,24 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
 
   // ---- epilogue: this workgroup's partial (tile t of wave wv: see gram_steps) ----
   double* out = a.partials + (int64_t)wg * a.stride;
-  constexpr int lo = G::lo_row(WV), hi = G::hi_row(WV);
 #pragma unroll
-  for (int k = 0; k < G::ntiles(WV); ++k) {
-    const int bi = k <= lo ? lo : hi, bj = k <= lo ? k : k - lo - 1;
+  for (int k = 0; k < TK::NT; ++k) {
+    const int sg = TK::seg_of(k);
+    const int bi = TK::row(sg), bj = TK::j0(sg) + k - TK::off(sg);
     const int t = bi * (bi + 1) / 2 + bj;
 #pragma unroll
     for (int j = 0; j < 4; ++j) out[t * 256 + 64 * j + lane] = acc[k][j];
   }
-  xz_lo += __shfl_xor(xz_lo, 16);
-  xz_lo += __shfl_xor(xz_lo, 32);
-  xz_hi += __shfl_xor(xz_hi, 16);
-  xz_hi += __shfl_xor(xz_hi, 32);
-  if (lane < 16) {
-    out[G::T * 256 + 16 * lo + lane] = xz_lo;
-    out[G::T * 256 + 16 * hi + lane] = xz_hi;
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    if constexpr (true) {
+      if (TK::diag(sg)) {
+        double v = xz[sg];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16) out[G::T * 256 + 16 * TK::row(sg) + lane] = v;
+      }
+    }
   }
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -446,22 +557,6 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
 // (16 tiles) + tile (7, g) of block row 7.  Other P16 (the mid-width generalisation): the tile
 // rows taken in pairs (0, P16-1), (1, P16-2), ... -- P16 + 1 tiles a pair -- and that sequence of
 // tiles cut into 8 equal contiguous runs, one per Gram wave (at most NSEG segments each).
-template <int P16>
-struct TileSeq {
-  static constexpr int T = P16 * (P16 + 1) / 2;
-  static constexpr int seq_row(int i) { return (i & 1) ? P16 - 1 - (i >> 1) : (i >> 1); }  // i-th row of the sequence
-  static constexpr int seq_start(int i) {  // first sequence index of row seq_row(i)
-    int t = 0;
-    for (int k = 0; k < i; ++k) t += seq_row(k) + 1;
-    return t;
-  }
-  static constexpr int seq_of(int t) {  // sequence row holding sequence tile t
-    int i = 0;
-    while (i + 1 < P16 && seq_start(i + 1) <= t) ++i;
-    return i;
-  }
-};
-constexpr int NSEG = 4;
 template <int P16, int WV>
 struct TilesR {
   static constexpr bool ROW = WV >= 8;

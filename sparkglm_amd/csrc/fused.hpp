@@ -27,7 +27,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 template <int P16>
 struct Geo {
   static_assert(P16 >= 2, "column-block count");  // odd counts: the layout of K1r only
-  static constexpr int NW = P16 / 2;               // waves per workgroup (K1: even P16)
+  // waves per workgroup: P16 / 2 (whole row pairs); P16 = 6 four (K1 takes its tiles as runs, so the
+  // wave count is free there): three 4-wave workgroups fit the LDS -- 12 waves, 3 per SIMD, where
+  // three 3-wave workgroups left one SIMD a third wave (p = 96 8.49 -> 7.93 ms, p = 80 9.39 -> 9.15,
+  // profiles/r04_midp_ab_run7_nw4.txt)
+  static constexpr int NW = P16 == 6 ? 4 : P16 / 2;
   static constexpr int NC = P16 * 16;              // padded columns
   static constexpr int NCE = (NC + 31) / 32 * 32;  // columns in the LDS image (eta stripes)
   static constexpr int T = P16 * (P16 + 1) / 2;    // lower-triangular 16x16 tiles
@@ -521,13 +525,13 @@ __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD))
   __syncthreads();
   switch (wv) {
     case 0: pass_body<P16, FAM, LNK, 0>(lds, a, wv, lane); break;
-    case 1: if constexpr (P16 >= 4) pass_body<P16, FAM, LNK, 1>(lds, a, wv, lane); break;
-    case 2: if constexpr (P16 >= 6) pass_body<P16, FAM, LNK, 2>(lds, a, wv, lane); break;
-    case 3: if constexpr (P16 >= 8) pass_body<P16, FAM, LNK, 3>(lds, a, wv, lane); break;
-    case 4: if constexpr (P16 >= 10) pass_body<P16, FAM, LNK, 4>(lds, a, wv, lane); break;
-    case 5: if constexpr (P16 >= 12) pass_body<P16, FAM, LNK, 5>(lds, a, wv, lane); break;
-    case 6: if constexpr (P16 >= 14) pass_body<P16, FAM, LNK, 6>(lds, a, wv, lane); break;
-    default: if constexpr (P16 >= 16) pass_body<P16, FAM, LNK, 7>(lds, a, wv, lane); break;
+    case 1: if constexpr (G::NW > 1) pass_body<P16, FAM, LNK, 1>(lds, a, wv, lane); break;
+    case 2: if constexpr (G::NW > 2) pass_body<P16, FAM, LNK, 2>(lds, a, wv, lane); break;
+    case 3: if constexpr (G::NW > 3) pass_body<P16, FAM, LNK, 3>(lds, a, wv, lane); break;
+    case 4: if constexpr (G::NW > 4) pass_body<P16, FAM, LNK, 4>(lds, a, wv, lane); break;
+    case 5: if constexpr (G::NW > 5) pass_body<P16, FAM, LNK, 5>(lds, a, wv, lane); break;
+    case 6: if constexpr (G::NW > 6) pass_body<P16, FAM, LNK, 6>(lds, a, wv, lane); break;
+    default: if constexpr (G::NW > 7) pass_body<P16, FAM, LNK, 7>(lds, a, wv, lane); break;
   }
 }
 

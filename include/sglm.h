@@ -194,6 +194,8 @@ typedef struct {
   char pass_kernel_name[64];/* that kernel's name as rocprofv3 lists it, e.g. "irls_pass_r_kernel<16,binomial,logit>" */
   int64_t lm_device_fits;   /* LM fits done in one device round trip (Gram pass, device Cholesky, residual pass;
                                resident p <= 64 shards without a communicator; SGLM_LM_DEVICE=0 disables) */
+  int64_t lm_device_reruns; /* of those, fits whose device coefficients were not the host solve's bit for bit (the
+                               host left Cholesky for LU): the residual pass reran at the host's coefficients */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device

@@ -64,7 +64,7 @@ class Stats(C.Structure):
                 ("overlap_chunks", C.c_int), ("comm_path", C.c_int), ("rank_blocks", C.c_int),
                 ("pass_kernel_ms_min", C.c_double), ("proc_chunks", C.c_int), ("proc_chunk_rows", C.c_int64),
                 ("solve_path", C.c_int), ("pass_kernel", C.c_int), ("pass_kernel_name", C.c_char * 64),
-                ("lm_device_fits", C.c_int64)]
+                ("lm_device_fits", C.c_int64), ("lm_device_reruns", C.c_int64)]
 
 
 COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}

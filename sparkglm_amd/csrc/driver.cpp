@@ -244,6 +244,7 @@ int lm_drive(Backend& be, sglm_prelm* out) {
   if (!dev || std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
     rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
     if (rc) return rc;
+    if (dev) be.lm_device_reruns += 1;
   }
   const double sse = s[S_DEV], top = s[S_PEARSON], bot = s[S_LL];
   const double r2 = top / bot;                                                      // LM.scala:185

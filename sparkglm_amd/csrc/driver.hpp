@@ -85,6 +85,7 @@ class Backend {
   virtual std::unique_ptr<SolverIface> make_solver(int64_t p) { return std::make_unique<HostSolver>(p); }
   // host-side timers (ms) for sglm_stats
   double solve_ms = 0.0;
+  int64_t lm_device_reruns = 0;  // device LM fits whose coefficients were not the host solve's (residual pass rerun)
   int solve_path = -1;  // enum sglm_solve_path of the last solve
 };
 

@@ -715,7 +715,7 @@ struct sglm_engine : public Backend {
       HIPCHK(hipMalloc(&dred, sizeof(double) * need_red));
       HIPCHK(hipMalloc(&dbeta, sizeof(double) * need_red));
       HIPCHK(hipHostMalloc(&hred, sizeof(double) * need_red, hipHostMallocDefault));
-      HIPCHK(hipHostMalloc(&hbeta, sizeof(double) * need_red, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&hbeta, sizeof(double) * need_red, hipHostMallocDefault));
       red_cap = need_red;
     }
     return ensure_small(64);
@@ -1355,8 +1355,11 @@ struct sglm_engine : public Backend {
     a.partials = dpart;
     const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
     HIPCHK(launch_stats(a, nb, st));
-    HIPCHK(launch_reduce_stats(dpart, nb, dstat, st));
-    HIPCHK(hipMemcpyAsync(hred, dred, sizeof(double) * (plen + NS + p), hipMemcpyDeviceToHost, st));
+    // the statistics sum also writes the whole result buffer into hred (pinned, device-visible): no
+    // copy blit after it
+    double* hred_dev = nullptr;
+    HIPCHK(hipHostGetDevicePointer((void**)&hred_dev, hred, 0));
+    HIPCHK(launch_reduce_stats(dpart, nb, dstat, st, dred, hred_dev, plen + NS + p));
     HIPCHK(hipStreamSynchronize(st));
     if (timed) {
       if (int rc = pass_timing()) return rc;
@@ -2277,6 +2280,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->solve_path = h->solve_path;
   out->pass_kernel = h->last_kernel;
   out->lm_device_fits = h->lm_device_fits;
+  out->lm_device_reruns = h->lm_device_reruns;
   std::memcpy(out->pass_kernel_name, h->last_kernel_name, sizeof out->pass_kernel_name);
   return SGLM_OK;
 }
@@ -2284,7 +2288,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
-  h->passes = h->dev_passes = h->lm_device_fits = 0;
+  h->passes = h->dev_passes = h->lm_device_fits = h->lm_device_reruns = 0;
   h->pass_ms = h->reduce_ms = h->last_pass_ms = h->last_reduce_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;

@@ -27,11 +27,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 template <int P16>
 struct Geo {
   static_assert(P16 >= 2, "column-block count");  // odd counts: the layout of K1r only
-  // waves per workgroup: P16 / 2 (whole row pairs); P16 = 6 four (K1 takes its tiles as runs, so the
-  // wave count is free there): three 4-wave workgroups fit the LDS -- 12 waves, 3 per SIMD, where
+  // waves per workgroup: P16 / 2 (whole row pairs; P16 = 16); P16 = 5..8 four (K1 takes its tiles as
+  // runs, so the wave count is free there): P16 = 5, 6: three 4-wave workgroups fit the LDS -- 12
+  // waves, 3 per SIMD, where
   // three 3-wave workgroups left one SIMD a third wave (p = 96 8.49 -> 7.93 ms, p = 80 9.39 -> 9.15,
   // profiles/r04_midp_ab_run7_nw4.txt)
-  static constexpr int NW = P16 == 6 ? 4 : P16 / 2;
+  static constexpr int NW = P16 >= 5 && P16 <= 8 ? 4 : P16 / 2;
   static constexpr int NC = P16 * 16;              // padded columns
   static constexpr int NCE = (NC + 31) / 32 * 32;  // columns in the LDS image (eta stripes)
   static constexpr int T = P16 * (P16 + 1) / 2;    // lower-triangular 16x16 tiles
@@ -504,7 +505,6 @@ __device__ __forceinline__ void pass_body(double* lds, const PassArgs& a, int wv
 template <int P16, int FAM, int LNK>
 __global__ void __launch_bounds__(64 * Geo<P16>::NW, (Geo<P16>::WAVES_PER_SIMD)) irls_pass_kernel(PassArgs a) {
   using G = Geo<P16>;
-  static_assert(P16 % 2 == 0, "K1: even column-block counts");
   __shared__ double lds[G::LDS_DOUBLES];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1054,6 +1054,29 @@ __global__ void __launch_bounds__(64 * GeoR<P16>::NW, 3) irls_pass_r_kernel(Pass
     case 10: pass_body_r<P16, FAM, LNK, 10>(lds, a, lane); break;
     default: pass_body_r<P16, FAM, LNK, 11>(lds, a, lane); break;
   }
+}
+
+// K1 launch for the family/link of the pass (LM passes: the Gaussian identity row stage).
+template <int P16>
+static hipError_t launch_pass_k1(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const dim3 g(grid), b(64 * Geo<P16>::NW);
+  const int mode_fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
+  const int mode_lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
+  if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, e0, e1, 0, a);
+  else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, e0, e1, 0, a);
+  else if (mode_fam == FAM_BINOMIAL)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, e0, e1, 0, a);
+  else if (mode_fam == FAM_GAUSSIAN)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, e0, e1, 0, a);
+  else if (mode_fam == FAM_POISSON)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, e0, e1, 0, a);
+  else if (mode_fam == FAM_GAMMA)
+    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, e0, e1, 0, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 // K1r launch for the family/link of the pass (LM passes: the Gaussian identity row stage).

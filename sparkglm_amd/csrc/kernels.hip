@@ -149,7 +149,12 @@ __global__ void ysum_kernel(const double* __restrict__ y, int64_t n, double* __r
 // of NS scalars per block, summed in a fixed order on the host side reduction.
 // One instantiation per family/link (as the pass kernels): an all-families kernel carried every
 // family's libm code (lgamma, erfinv, ...) at 438 VGPRs, one wave per SIMD, latency-bound.
-template <int FAM, int LNK>
+// PM > 0 (LM residuals on a resident shard, p <= PM, PM a multiple of 8): the row's p loads of X are
+// issued together -- every column slot loads (slots past p re-read column 0, a cache hit) and the
+// products enter eta branch-free -- where the runtime-p loop waited for each load before its fma
+// (configs[0]: 34 us for a 168 MB pass, one HBM latency per column).  The same fma chain, so the
+// same eta.
+template <int FAM, int LNK, int PM = 0>
 __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   __shared__ double red[4][NS];
   RowAcc acc;
@@ -158,11 +163,23 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
   const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = (lo + per < a.n) ? lo + per : a.n;
   const double ybar = a.ybar_dev ? *a.ybar_dev : a.ybar;
+  double bl[PM > 0 ? PM : 1];
+  if constexpr (PM > 0) {
+#pragma unroll
+    for (int j = 0; j < PM; ++j)
+      bl[j] = j >= a.p ? 0.0 : a.beta_by_value ? a.bv[j < STATS_BETA_MAX ? j : 0] : a.beta[j];
+  }
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const double m = a.m ? a.m[i] : 1.0;
     const double pw = a.prior ? a.prior[i] : 1.0;
     double eta = 0.0;
-    if (a.X) {  // LM residuals: X*coefs in predict_kernel's order (LM.scala:173-174)
+    if constexpr (PM > 0) {
+      double x[PM];
+#pragma unroll
+      for (int j = 0; j < PM; ++j) x[j] = a.X[(int64_t)(j < a.p ? j : 0) * a.ld + i];
+#pragma unroll
+      for (int j = 0; j < PM; ++j) eta = j < a.p ? fma(x[j], bl[j], eta) : eta;
+    } else if (a.X) {  // LM residuals: X*coefs in predict_kernel's order (LM.scala:173-174)
       if (a.beta_by_value)
         for (int j = 0; j < a.p; ++j) eta += a.X[(int64_t)j * a.ld + i] * a.bv[j];
       else
@@ -188,111 +205,97 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // LM.fit's p x p solve on the device (engine.cpp lm_device; p <= 64): the host solver's Cholesky
 // (solve.cpp chol_factor + chol_solve), element for element in the same operation order without
 // contraction, so the coefficients come out bitwise the host's (driver.cpp lm_drive checks that and
-// otherwise reruns the residual pass at its own).  Four waves; in every wave lane i is row i.
-// The factorization runs right-looking: step k takes column k's pivot and scales the column, then
-// subtracts L(i,k) L(j,k) from every trailing element (i, j) -- each element still receives its
-// subtractions in ascending k, exactly chol_factor's left-looking order, but one step's subtractions
-// are independent: waves 0-2 split the trailing columns (j mod 3), each forming the pivot and L(:,k)
-// itself (the same operations, so the same values) and taking L(j,k) from its own lanes by readlane;
-// wave 3 runs the forward sweep L t = b one column behind.  One barrier per step.  The back
-// substitution is a column sweep on one wave (the host chol_solve's order).  The first forms -- one
-// wave, left-looking, one LDS read and branch per subtraction -- took 37 us at p = 20; one wave
-// right-looking 26 us (the chain of 20 pivots at single-wave latency plus all the updates).
+// otherwise reruns the residual pass at its own).  One wave; lane i holds row i of the matrix in
+// registers (a[j] = A(i, j), PM = p rounded up to 8, every loop unrolled, no branch): step k reads
+// the pivot from lane k, scales column k (L(i, k) = A(i, k) / sqrt(d) as 1 / sqrt(d) times, the host's
+// order) and subtracts L(i, k) L(j, k) from A(i, j), j > k, with L(j, k) read from lane j -- each
+// element receives its subtractions in ascending k, chol_factor's left-looking order, and L(j, k) == 0
+// skips the subtraction as there.  The forward sweep L t = b runs in the same steps, the back
+// substitution L' x = t as a column sweep over L staged once in LDS (the host chol_solve's order).
+// Rows p..PM-1 are identity padding: their steps divide by 1 and subtract zeros, which leaves the real
+// rows' values unchanged (their t stays 0 and the back substitution skips them), so the whole
+// factorization is one basic block the compiler can overlap
+// across steps.  A pivot that is not positive and finite sets the failure flag (the host stops there;
+// the values past it are not used).  Earlier forms -- one wave in LDS, left-looking, 37 us at p = 20;
+// right-looking 26 us; four waves over LDS with a barrier a step 19 us -- were bound by the per-step
+// LDS round trips and barriers on the 20-pivot chain.
 // Out: beta[p]; aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where the host would leave
 // Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO: solve.cpp chol_pivot_ratio).
 __device__ __forceinline__ double lane_bcast(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
-__global__ void __launch_bounds__(256) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
-                                                      double* __restrict__ beta, double* __restrict__ aux) {
+template <int PM>
+__global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
+                                                     double* __restrict__ beta, double* __restrict__ aux) {
 #pragma clang fp contract(off)
-  constexpr int LD = 65, U = 8, NUPD = 3;  // A(r, c) at A[c LD + r]; waves 0..NUPD-1 update, wave NUPD solves
-  __shared__ double A[64 * LD], dg[64], tsh[64];
-  __shared__ int fail_sh;
-  const int i = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int LDL = PM + 1;
+  __shared__ double Ls[PM * LDL];  // L(r, c) at Ls[r LDL + c] for the back substitution
+  const int i = threadIdx.x;
   const bool row = i < p;
   const int64_t tri = (int64_t)p * (p + 1) / 2;
-  for (int e = threadIdx.x; e < p * p; e += 256) {  // unpack_gram: A(r, c) = packed[max(r, c) (max + 1) / 2 + min(r, c)]
-    const int r = e % p, c = e / p, hi = r > c ? r : c, lo = r > c ? c : r;
-    A[c * LD + r] = packed[hi * (hi + 1) / 2 + lo];
+  double a[PM];
+#pragma unroll
+  for (int j = 0; j < PM; ++j) {  // unpack_gram's lower triangle: A(i, j) = packed[i (i + 1) / 2 + j], j <= i
+    const bool in = row && j <= i;  // every lane loads (index 0 outside): no branch around the loads
+    const double v = packed[in ? (int64_t)i * (i + 1) / 2 + j : 0];
+    a[j] = in ? v : (i == j ? 1.0 : 0.0);
   }
-  if (threadIdx.x < 64 && row) dg[i] = packed[(int64_t)i * (i + 1) / 2 + i];
-  if (threadIdx.x == 0) fail_sh = 0;
-  double ti = row ? packed[tri + i] : 0.0;  // wave NUPD: the forward sweep's t
-  __syncthreads();
-  for (int k = 0; k < p; ++k) {  // chol_factor
-    const double d = A[k * LD + k];
-    const double aik = A[k * LD + i];
-    if (!(d > 0.0) || !isfinite(d)) {  // every wave sees the same d: a uniform exit
-      if (threadIdx.x == 0) fail_sh = 1;
-      break;
-    }
+  const double dgi = row ? packed[(int64_t)i * (i + 1) / 2 + i] : 0.0;
+  double ti = row ? packed[tri + i] : 0.0;
+  double diag = 1.0;
+  bool fail = false;
+#pragma unroll
+  for (int k = 0; k < PM; ++k) {
+    const double d = lane_bcast(a[k], k);
+    fail = fail || !(d > 0.0) || !isfinite(d);
     const double sq = sqrt(d);
-    const double inv = 1.0 / sq;
-    const double lik = (i == k) ? sq : aik * inv;  // L(i, k), lanes i >= k
-    if (wv < NUPD) {
-      // A(i, j) -= L(i, k) L(j, k) for this wave's trailing columns j = k+1+wv, k+1+wv+NUPD, ...; L(j, k) == 0 skipped
-      for (int j0 = k + 1 + wv; j0 < p; j0 += NUPD * U) {
-        double l[U], x[U];
+    double inv = 1.0 / sq;
+    asm volatile("" : "+v"(inv));  // formed on every lane, not in a branch around lane k (a step stays one block)
+    const double lik = (i == k) ? sq : a[k] * inv;  // L(i, k), lanes i >= k
+    const double tk = lane_bcast(ti / sq, k);      // L t = b: t_k /= L(k, k); t_i -= L(i, k) t_k, i > k
+    if (i > k && row) ti -= lik * tk;
+    if (i == k) ti = tk;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int j = j0 + NUPD * u < p ? j0 + NUPD * u : p - 1;
-          l[u] = lane_bcast(lik, j);
-          x[u] = A[j * LD + i];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int j = j0 + NUPD * u;
-          if (j < p) {  // wave-uniform
-            const double nv = x[u] - lik * l[u];
-            A[j * LD + i] = (i >= j && row && l[u] != 0.0) ? nv : x[u];
-          }
-        }
-      }
-    } else {
-      // L t = b, column k: t_k /= L(k, k); t_i -= L(i, k) t_k, i > k
-      const double tk = lane_bcast(ti / sq, k);
-      if (i == k) ti = tk;
-      if (i > k && row) ti -= lik * tk;
+    for (int j = k + 1; j < PM; ++j) {
+      const double l = lane_bcast(lik, j);
+      const double nv = a[j] - lik * l;
+      a[j] = (i >= j && l != 0.0) ? nv : a[j];
     }
-    __syncthreads();
-    // column k of L into A after every wave has read A(k, k) and A(:, k) (only the solves and the
-    // pivot ratio read it again; the next step reads column k + 1)
-    if (wv == 0 && i >= k && row) A[k * LD + i] = lik;
+    if (i >= k) a[k] = lik;
+    if (i == k) diag = sq;
   }
-  __syncthreads();
-  const int fail = fail_sh;
   if (!fail) {
-    if (wv == NUPD) tsh[i] = ti;
-    __syncthreads();
-    if (wv == 0) {
-      double tb = tsh[i];
-      for (int r = p - 1; r >= 0; --r) {  // L' x = t: x_r = t_r / L(r, r); t_i -= L(r, i) x_r, i < r
-        const double xr = lane_bcast(tb / A[i * LD + i], r);
-        if (i == r) tb = xr;
-        if (i < r) tb -= A[i * LD + r] * xr;
-      }
-      if (row) beta[i] = tb;
+    if (i < PM) {
+#pragma unroll
+      for (int j = 0; j < PM; ++j) Ls[i * LDL + j] = a[j];
     }
+    __syncthreads();
+    double tb = ti;
+#pragma unroll
+    for (int r = PM - 1; r >= 0; --r) {  // L' x = t: x_r = t_r / L(r, r); t_i -= L(r, i) x_r, i < r
+      const double xr = lane_bcast(tb / diag, r);
+      const double lri = Ls[r * LDL + (i < PM ? i : 0)];
+      tb = (i < r && r < p) ? tb - lri * xr : tb;  // padding rows stay out
+      if (i == r) tb = xr;
+    }
+    if (row) beta[i] = tb;
   }
-  if (threadIdx.x == 0) {
-    double r = 1.0;  // chol_pivot_ratio
-    if (!fail)
-      for (int j = 0; j < p; ++j) {
-        const double l = A[j * LD + j], a = dg[j];
-        if (a > 0.0) r = fmin(r, (l * l) / a);
-      }
+  double r = (row && dgi > 0.0) ? (diag * diag) / dgi : 1.0;  // chol_pivot_ratio: min over j (exact, any order)
+  for (int o = 1; o < 64; o <<= 1) r = fmin(r, __shfl_xor(r, o));
+  if (i == 0) {
     aux[0] = packed[tri + p + S_DEV] / packed[tri + p + S_SUMW];
-    aux[1] = (fail || r < ratio_min) ? 1.0 : 0.0;
+    aux[1] = (fail || fmin(1.0, r) < ratio_min) ? 1.0 : 0.0;
   }
 }
 
 // The stats partials [nparts][NS] summed on the device into out[NS] (no D2H of the partials):
 // thread (segment s, scalar k) sums partials [s n / 32, (s+1) n / 32) in order, Neumaier-compensated,
 // then thread k adds the 32 segment sums and their compensations in segment order.
+// host != null (the LM device round trip): the kernel also writes the fit's result buffer into pinned
+// host memory -- src[0, ncopy) with out at src + out_off -- so no copy blit follows it (~4 us).
 __global__ void __launch_bounds__(256) reduce_stats_kernel(const double* __restrict__ part, int nparts,
-                                                           double* __restrict__ out) {
+                                                           double* __restrict__ out, const double* __restrict__ src,
+                                                           double* __restrict__ host, int64_t ncopy, int64_t out_off) {
   __shared__ double ss[32][NS], cs[32][NS];
   const int k = threadIdx.x % NS, sg = threadIdx.x / NS;
   const int g0 = (int)((int64_t)nparts * sg / 32), g1 = (int)((int64_t)nparts * (sg + 1) / 32);
@@ -316,7 +319,11 @@ __global__ void __launch_bounds__(256) reduce_stats_kernel(const double* __restr
       tc += cs[q][threadIdx.x];
     }
     out[threadIdx.x] = t + tc;
+    if (host) host[out_off + threadIdx.x] = t + tc;
   }
+  if (host)
+    for (int64_t e = threadIdx.x; e < ncopy; e += blockDim.x)
+      if (e < out_off || e >= out_off + NS) host[e] = src[e];
 }
 
 // ---------------------------------------------------------------------------------
@@ -374,13 +381,17 @@ __global__ void synth_kernel(int kind, int64_t row0, int64_t n, int p, uint64_t 
 // Its DMA addresses the 4 columns of a quad by 32-bit lane offsets (3 ld + 32 rows, in bytes),
 // which bounds the shard at ~178M rows.
 constexpr int K1R_MIN_P16 = 10, K1R_MIN_ODD = 9;
+// K1 runs the odd counts 5 and 7 itself (its tiles are runs of the tile sequence, not row pairs:
+// p = 65..80 and 97..112 run 15 / 28 tiles instead of 21 / 36); above, an odd count K1r may not run
+// rounds up to K1's even one.
+constexpr int K1_MAX_ODD = 7;
 bool pass_uses_split(int P16, int fused_split, int64_t ld) {
   const int thr = fused_split == 1 ? ((P16 & 1) ? K1R_MIN_ODD : K1R_MIN_P16) : fused_split;
   return fused_split != 0 && P16 >= 5 && P16 >= thr && ld * 24 + 4096 < ((int64_t)1 << 32);
 }
 int pass_variant(int p, int fused_split, int64_t ld) {
   int P16 = (p + 15) / 16;
-  if ((P16 & 1) && !pass_uses_split(P16, fused_split, ld)) ++P16;
+  if ((P16 & 1) && P16 > K1_MAX_ODD && !pass_uses_split(P16, fused_split, ld)) ++P16;
   return P16 < 2 ? 2 : P16;
 }
 int pass_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS; }
@@ -393,7 +404,9 @@ int pass_wg_per_cu(int P16) {
   switch (P16) {
     case 2: return wg_per_cu_t<2>();
     case 4: return wg_per_cu_t<4>();
+    case 5: return wg_per_cu_t<5>();
     case 6: return wg_per_cu_t<6>();
+    case 7: return wg_per_cu_t<7>();
     case 8: return wg_per_cu_t<8>();
     case 10: return wg_per_cu_t<10>();
     case 12: return wg_per_cu_t<12>();
@@ -404,35 +417,13 @@ int pass_wg_per_cu(int P16) {
 
 template <int P16>
 static hipError_t launch_pass_p(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  static_assert(P16 % 2 == 0, "K1: even column-block counts (odd ones: fused_odd.hip)");
   if constexpr (P16 >= 6)
     if (pass_uses_split(P16, a.fused_split, a.ld)) return launch_pass_r_fl<P16>(a, grid, st, e0, e1);
-  const dim3 g(grid), b(64 * Geo<P16>::NW);
-  const int mode_fam = (a.mode == MODE_LM_GRAM) ? FAM_GAUSSIAN : a.family;
-  const int mode_lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
-  if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_LOGIT)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_LOGIT>), g, b, 0, st, e0, e1, 0, a);
-  else if (mode_fam == FAM_BINOMIAL && mode_lnk == LNK_PROBIT)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_PROBIT>), g, b, 0, st, e0, e1, 0, a);
-  else if (mode_fam == FAM_BINOMIAL)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_BINOMIAL, LNK_CLOGLOG>), g, b, 0, st, e0, e1, 0, a);
-  else if (mode_fam == FAM_GAUSSIAN)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAUSSIAN, LNK_IDENTITY>), g, b, 0, st, e0, e1, 0, a);
-  else if (mode_fam == FAM_POISSON)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_POISSON, LNK_LOG>), g, b, 0, st, e0, e1, 0, a);
-  else if (mode_fam == FAM_GAMMA)
-    hipExtLaunchKernelGGL((irls_pass_kernel<P16, FAM_GAMMA, LNK_INVERSE>), g, b, 0, st, e0, e1, 0, a);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
+  return launch_pass_k1<P16>(a, grid, st, e0, e1);
 }
 
 hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if ((P16 & 1) && P16 >= 5) {
-    // odd counts exist only as K1r: refuse a pass that may not run it (pass_variant rounds those up)
-    if (!pass_uses_split(P16, a.fused_split, a.ld)) return hipErrorInvalidValue;
-    return launch_pass_odd(P16, a, grid, st, e0, e1);
-  }
+  if ((P16 & 1) && P16 >= 5) return launch_pass_odd(P16, a, grid, st, e0, e1);  // fused_odd.hip
   switch (P16) {
     case 2: return launch_pass_p<2>(a, grid, st, e0, e1);
     case 4: return launch_pass_p<4>(a, grid, st, e0, e1);
@@ -448,18 +439,40 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hip
 
 hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st) {
   if (p < 1 || p > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lm_chol_kernel, dim3(1), dim3(256), 0, st, packed, p, ratio_min, beta, aux);
+  switch ((p + 7) / 8) {  // PM = p rounded up to 8 (identity padding)
+    case 1: hipLaunchKernelGGL(lm_chol_kernel<8>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 2: hipLaunchKernelGGL(lm_chol_kernel<16>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 3: hipLaunchKernelGGL(lm_chol_kernel<24>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 4: hipLaunchKernelGGL(lm_chol_kernel<32>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 5: hipLaunchKernelGGL(lm_chol_kernel<40>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 6: hipLaunchKernelGGL(lm_chol_kernel<48>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    case 7: hipLaunchKernelGGL(lm_chol_kernel<56>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    default: hipLaunchKernelGGL(lm_chol_kernel<64>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(32 * NS), 0, st, part, nparts, out);
+hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st, const double* src,
+                               double* host, int64_t ncopy) {
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(32 * NS), 0, st, part, nparts, out, src, host, ncopy,
+                     (int64_t)(out - src));
   return hipGetLastError();
 }
 
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
   const dim3 gr(grid), bl(256);
-  if (a.mode == MODE_LM_RESID || (a.family == FAM_GAUSSIAN && a.link == LNK_IDENTITY))
+  if (a.X && a.mode == MODE_LM_RESID && a.p >= 1 && a.p <= 64) {  // the LM residual pass, loads together
+    switch ((a.p + 7) / 8) {
+      case 1: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 8>), gr, bl, 0, st, a); break;
+      case 2: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 16>), gr, bl, 0, st, a); break;
+      case 3: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 24>), gr, bl, 0, st, a); break;
+      case 4: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 32>), gr, bl, 0, st, a); break;
+      case 5: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 40>), gr, bl, 0, st, a); break;
+      case 6: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 48>), gr, bl, 0, st, a); break;
+      case 7: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 56>), gr, bl, 0, st, a); break;
+      default: hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY, 64>), gr, bl, 0, st, a); break;
+    }
+  } else if (a.mode == MODE_LM_RESID || (a.family == FAM_GAUSSIAN && a.link == LNK_IDENTITY))
     hipLaunchKernelGGL((stats_kernel<FAM_GAUSSIAN, LNK_IDENTITY>), gr, bl, 0, st, a);
   else if (a.family == FAM_BINOMIAL && a.link == LNK_LOGIT)
     hipLaunchKernelGGL((stats_kernel<FAM_BINOMIAL, LNK_LOGIT>), gr, bl, 0, st, a);

@@ -20,7 +20,9 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hip
                        hipEvent_t e1 = nullptr);
 hipError_t launch_pass_odd(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1);  // fused_odd.hip: K1r, P16 5..15 odd
 hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
-hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st);  // [nparts][NS] -> [NS]
+// [nparts][NS] -> [NS]; host != null: also src[0, ncopy) (out inside it) into host memory the device can write
+hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st, const double* src = nullptr,
+                               double* host = nullptr, int64_t ncopy = 0);
 // LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}
 hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st);
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st,

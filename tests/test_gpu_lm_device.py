@@ -36,7 +36,8 @@ def _fits(load):
         with _engine(device) as e:
             load(e)
             f = e.fit_lm()
-            out[device] = (f, e.stats()["lm_device_fits"])
+            st = e.stats()
+            out[device] = (f, st["lm_device_fits"], st["lm_device_reruns"])
     return out
 
 
@@ -50,8 +51,8 @@ def _same(a, b):
 def test_config0_design_bitwise_the_host_path_and_the_oracle():
     n, p = 1_000_000, 20
     res = _fits(lambda e: e.synth(1, 0, n, p, 1))
-    (fd, nd), (fh, nh) = res[True], res[False]
-    assert nd == 1 and nh == 0
+    (fd, nd, rd), (fh, nh, _) = res[True], res[False]
+    assert nd == 1 and nh == 0 and rd == 0  # the device Cholesky's coefficients were the host's, bitwise
     _same(fd, fh)
     X, y, _, _ = synth.generate(1, 0, n, p, 1)
     r = po.fit_lm(X, y, nthreads=8)
@@ -59,14 +60,14 @@ def test_config0_design_bitwise_the_host_path_and_the_oracle():
     assert rel([fd.sse, fd.r2, fd.fstat, fd.sigma], [r["sse"], r["r2"], r["fstat"], r["sigma"]]) < 1e-9
 
 
-@pytest.mark.parametrize("p", [1, 7, 33, 64])
+@pytest.mark.parametrize("p", [1, 7, 8, 9, 20, 33, 48, 57, 64])
 def test_widths_bitwise_the_host_path(p):
     rng = np.random.default_rng(p)
     n = 50_001
     X = np.column_stack([np.ones(n), rng.uniform(-1, 1, (n, p - 1))]) if p > 1 else np.ones((n, 1))
     y = X @ rng.normal(size=p) + rng.uniform(-1, 1, n)
     res = _fits(lambda e: e.set_data(X, y))
-    assert res[True][1] == 1
+    assert res[True][1] == 1 and res[True][2] == 0  # device coefficients bitwise the host solve's
     _same(res[True][0], res[False][0])
 
 
@@ -79,6 +80,7 @@ def test_ill_conditioned_falls_back_to_the_host_lu():
     X = np.column_stack([np.ones(n), x1, x1 + 1e-5 * rng.uniform(-1, 1, n), rng.uniform(-1, 1, (n, 3))])
     y = X @ np.array([1.0, 2.0, -1.0, 0.5, 0.25, -0.75]) + rng.uniform(-1, 1, n)
     res = _fits(lambda e: e.set_data(X, y))
+    assert res[True][1] == 1 and res[True][2] == 1  # flagged on the device, rerun at the LU coefficients
     _same(res[True][0], res[False][0])
     r = po.fit_lm(X, y)
     assert rel(res[True][0].sse, r["sse"]) < 1e-9

@@ -1,8 +1,9 @@
 """The engine's kernel choice (sglm_pass_kernel_for: the rule ensure_workspace / launch_pass /
 launch_narrow apply, and the label of bench.py's roofline line) -- on the CPU, no device touched:
 narrow for p <= 64; the fused pass for 65 <= p <= 256: P16 = ceil(p / 16) column blocks, split-role K1r
-from P16 = 10 and at every odd P16 >= 9 (K1 is built for even counts only: an odd count that may not
-run K1r rounds up to K1's next even one; SGLM_FUSED_SPLIT = 5 / 7 opens the odd counts below) unless SGLM_FUSED_SPLIT moves or disables the threshold, and K1 again when
+from P16 = 10 and at every odd P16 >= 9; K1 below, at odd 5 and 7 too (its tiles are runs of the tile
+sequence); an odd count >= 9 that may not run K1r rounds up to K1's next even one; SGLM_FUSED_SPLIT =
+5 / 7 puts K1r on the odd counts below) unless SGLM_FUSED_SPLIT moves or disables the threshold, and K1 again when
 the shard is too tall for K1r's 32-bit DMA lane offsets (ld * 24 + 4096 >= 2^32, ~179M rows); the
 wide path above p = 256, for procedural shards and under SGLM_FORCE_WIDE."""
 import pytest
@@ -14,13 +15,14 @@ from sparkglm_amd import _lib as L
     (1_000_000, 20, 1, False, False, "narrow", "irls_narrow_kernel<2,binomial,logit>"),
     (1_000_000_000, 32, 1, False, False, "narrow", "irls_narrow_kernel<2,binomial,logit>"),
     (125_000_000, 64, 1, False, False, "narrow", "irls_narrow_kernel<4,binomial,logit>"),
-    (10_000_000, 65, 1, False, False, "fused", "irls_pass_kernel<6,binomial,logit>"),
-    (10_000_000, 80, 1, False, False, "fused", "irls_pass_kernel<6,binomial,logit>"),
+    (10_000_000, 65, 1, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),
+    (10_000_000, 80, 1, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),
     (10_000_000, 80, 5, False, False, "fused-split", "irls_pass_r_kernel<5,binomial,logit>"),
     (10_000_000, 81, 1, False, False, "fused", "irls_pass_kernel<6,binomial,logit>"),
-    (10_000_000, 80, 0, False, False, "fused", "irls_pass_kernel<6,binomial,logit>"),  # K1 only: rounded up
-    (10_000_000, 80, 6, False, False, "fused-split", "irls_pass_r_kernel<6,binomial,logit>"),
-    (10_000_000, 112, 1, False, False, "fused", "irls_pass_kernel<8,binomial,logit>"),
+    (10_000_000, 80, 0, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),  # K1 runs odd 5 / 7
+    (10_000_000, 80, 6, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),  # K1r from 6: K1 at odd 5
+    (10_000_000, 96, 6, False, False, "fused-split", "irls_pass_r_kernel<6,binomial,logit>"),
+    (10_000_000, 112, 1, False, False, "fused", "irls_pass_kernel<7,binomial,logit>"),
     (10_000_000, 112, 7, False, False, "fused-split", "irls_pass_r_kernel<7,binomial,logit>"),
     (10_000_000, 144, 1, False, False, "fused-split", "irls_pass_r_kernel<9,binomial,logit>"),
     (10_000_000, 128, 1, False, False, "fused", "irls_pass_kernel<8,binomial,logit>"),

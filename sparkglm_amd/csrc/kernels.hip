@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // (solve.cpp chol_factor + chol_solve), element for element in the same operation order without
 // contraction, so the coefficients come out bitwise the host's (driver.cpp lm_drive checks that and
 // otherwise reruns the residual pass at its own).  One wave; lane i holds row i of the matrix in
-// registers (a[j] = A(i, j), PM = p rounded up to 8, every loop unrolled, no branch): step k reads
+// registers (a[j] = A(i, j), PM = p rounded up to 4 / 8, every loop unrolled, no branch): step k reads
 // the pivot from lane k, scales column k (L(i, k) = A(i, k) / sqrt(d) as 1 / sqrt(d) times, the host's
 // order) and subtracts L(i, k) L(j, k) from A(i, j), j > k, with L(j, k) read from lane j -- each
 // element receives its subtractions in ascending k, chol_factor's left-looking order, and L(j, k) == 0
@@ -439,15 +439,15 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hip
 
 hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st) {
   if (p < 1 || p > 64) return hipErrorInvalidValue;
-  switch ((p + 7) / 8) {  // PM = p rounded up to 8 (identity padding)
-    case 1: hipLaunchKernelGGL(lm_chol_kernel<8>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 2: hipLaunchKernelGGL(lm_chol_kernel<16>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 3: hipLaunchKernelGGL(lm_chol_kernel<24>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 4: hipLaunchKernelGGL(lm_chol_kernel<32>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 5: hipLaunchKernelGGL(lm_chol_kernel<40>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 6: hipLaunchKernelGGL(lm_chol_kernel<48>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    case 7: hipLaunchKernelGGL(lm_chol_kernel<56>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
-    default: hipLaunchKernelGGL(lm_chol_kernel<64>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+  // PM = p rounded up to 4 up to 32, to 8 above (identity padding: a padding step costs what a real one does)
+  const int pm = p <= 32 ? (p + 3) / 4 * 4 : (p + 7) / 8 * 8;
+  switch (pm) {
+#define SGLM_CHOL_CASE(PM) \
+  case PM: hipLaunchKernelGGL(lm_chol_kernel<PM>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+    SGLM_CHOL_CASE(4) SGLM_CHOL_CASE(8) SGLM_CHOL_CASE(12) SGLM_CHOL_CASE(16) SGLM_CHOL_CASE(20) SGLM_CHOL_CASE(24)
+    SGLM_CHOL_CASE(28) SGLM_CHOL_CASE(32) SGLM_CHOL_CASE(40) SGLM_CHOL_CASE(48) SGLM_CHOL_CASE(56) SGLM_CHOL_CASE(64)
+#undef SGLM_CHOL_CASE
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

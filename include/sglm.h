@@ -55,10 +55,11 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 6  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
+#define SGLM_ABI_VERSION 7  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
                               sglm_stats.comm_path / rank_blocks / pass_kernel_ms_min / proc_chunks /
                               proc_chunk_rows / solve_path; 6: sglm_stats.pass_kernel / pass_kernel_name,
-                              sglm_set_comm_rank collective */
+                              sglm_set_comm_rank collective; 7: sglm_stats.lm_device_fits /
+                              lm_device_reruns */
 
 enum sglm_status {
   SGLM_OK = 0,

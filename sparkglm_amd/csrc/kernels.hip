@@ -36,7 +36,7 @@ namespace sglm {
 // p = 20 LM Gram has 238 outputs: one chain over all partials each was a latency-bound 15 us).
 // The scalars (deviance, ...) are Neumaier-compensated at both levels.
 // ---------------------------------------------------------------------------------
-constexpr int RED_SEG = 8, RED_EL = 256 / RED_SEG;
+constexpr int RED_SEG = 8, RED_EL = 256 / RED_SEG, RED_BATCH = 32;
 
 __global__ void __launch_bounds__(256) reduce_partials_kernel(const double* __restrict__ part, int64_t stride,
                                                               int nparts, int p, int P16, double* __restrict__ out) {
@@ -66,25 +66,26 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(const double* __re
       } else {
         src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
       }
-      // the segment's partials left to right, 8 loads in flight per thread
+      // the segment's partials left to right, RED_BATCH loads in flight per thread (a 256-partial
+      // reduce is one batch: one load latency, not four)
       const double* q = part + src;
       int g = g0;
       if (!scal) {
-        for (; g + 8 <= g1; g += 8) {
-          double v[8];
+        for (; g + RED_BATCH <= g1; g += RED_BATCH) {
+          double v[RED_BATCH];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = q[(int64_t)(g + u) * stride];
+          for (int u = 0; u < RED_BATCH; ++u) v[u] = q[(int64_t)(g + u) * stride];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) s += v[u];
+          for (int u = 0; u < RED_BATCH; ++u) s += v[u];
         }
         for (; g < g1; ++g) s += q[(int64_t)g * stride];
       } else {  // deviance and the other scalars: compensated, in the same order
-        for (; g + 8 <= g1; g += 8) {
-          double v[8];
+        for (; g + RED_BATCH <= g1; g += RED_BATCH) {
+          double v[RED_BATCH];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = q[(int64_t)(g + u) * stride];
+          for (int u = 0; u < RED_BATCH; ++u) v[u] = q[(int64_t)(g + u) * stride];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) neumaier_add(s, c, v[u]);
+          for (int u = 0; u < RED_BATCH; ++u) neumaier_add(s, c, v[u]);
         }
         for (; g < g1; ++g) neumaier_add(s, c, q[(int64_t)g * stride]);
       }
@@ -301,12 +302,12 @@ __global__ void __launch_bounds__(256) reduce_stats_kernel(const double* __restr
   const int g0 = (int)((int64_t)nparts * sg / 32), g1 = (int)((int64_t)nparts * (sg + 1) / 32);
   double s = 0.0, c = 0.0;
   int g = g0;
-  for (; g + 8 <= g1; g += 8) {  // 8 loads in flight ahead of the ordered compensated adds
-    double v[8];
+  for (; g + RED_BATCH <= g1; g += RED_BATCH) {  // RED_BATCH loads in flight ahead of the ordered compensated adds
+    double v[RED_BATCH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(g + u) * NS + k];
+    for (int u = 0; u < RED_BATCH; ++u) v[u] = part[(int64_t)(g + u) * NS + k];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) neumaier_add(s, c, v[u]);
+    for (int u = 0; u < RED_BATCH; ++u) neumaier_add(s, c, v[u]);
   }
   for (; g < g1; ++g) neumaier_add(s, c, part[(int64_t)g * NS + k]);
   ss[sg][k] = s;

@@ -1318,6 +1318,12 @@ struct sglm_engine : public Backend {
     return SGLM_OK;
   }
 
+  // blocks (= partials) of the statistics pass; the LM device round trip and the host path alike
+  // (LM 1M x 20: 2048 blocks measured equal, 4096 +5 %: profiles/r04_lm_stats_blocks.txt)
+  static int stats_blocks(int64_t rows) {
+    return (int)std::min<int64_t>(4096, std::max<int64_t>(1024, rows / 131072));
+  }
+
   // LM.fit in one round trip (driver.hpp Backend::lm_device): a resident narrow shard with no
   // communicator -- the Gram pass, lm_chol_kernel (the host Cholesky, bitwise, on the device), the
   // residual pass at its coefficients (beta and ybar read from the device) and the device sum of its
@@ -1353,7 +1359,7 @@ struct sglm_engine : public Backend {
     a.link = LNK_IDENTITY;
     a.mode = MODE_LM_RESID;
     a.partials = dpart;
-    const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
+    const int nb = stats_blocks(n);
     HIPCHK(launch_stats(a, nb, st));
     // the statistics sum also writes the whole result buffer into hred (pinned, device-visible): no
     // copy blit after it
@@ -1431,7 +1437,7 @@ struct sglm_engine : public Backend {
     // one wave per SIMD leaves the per-row chain latency-bound on large shards; small ones
     // (LM 1M x 20) keep 1024 partials; they are summed on the device (reduce_stats_kernel,
     // compensated) and only the NS sums come back
-    const int nb = (int)std::min<int64_t>(4096, std::max<int64_t>(1024, n / 131072));
+    const int nb = stats_blocks(n);
     HIPCHK(launch_stats(a, nb, st));
     if (int rc = ensure_small(64)) return rc;
     HIPCHK(launch_reduce_stats(dpart, nb, dsmall, st));

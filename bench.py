@@ -127,6 +127,27 @@ def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
         return None
 
 
+def pmc_traffic_source(p: int, n: int, family: str, procedural: bool = False):
+    """Where `roofline.traffic` comes from: it is NOT a counter of the timed run but a stored
+    rocprofv3 --pmc measurement (bytes per row of a profiling pass over `measured_rows` rows of the
+    same shape) scaled to this launch's rows."""
+    e = pmc_entry(p, family, procedural)
+    if e is None or "bytes_per_row" not in e:
+        return None
+    key = f"{family}:{p}" + (":proc" if procedural else "")
+    tab_key = key if key in _pmc_table() else str(p)
+    return (f"stored PMC, profiles/pmc_traffic.json[{tab_key!r}]: {e['bytes_per_row']:.2f} B/row measured over "
+            f"{e.get('measured_rows')} rows ({e.get('source', '?')}), x {n} rows of this launch")
+
+
+def _pmc_table() -> dict:
+    try:
+        with open(os.path.join(HERE, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def mfma_clock_bound(p: int, n: int, family: str, procedural: bool = False) -> dict:
     """The fp64 MFMA instruction stream of a pass -- the second resource of an HBM-bound pass, the
     bound of an MFMA-bound one: the lower-triangular 16x16 tile grid, one v_mfma_f64_16x16x4 per
@@ -301,16 +322,18 @@ def main() -> int:
         tflops = flops / (kern_ms * 1e-3) / 1e12
         gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
         traffic = pmc_traffic(p, n, fam, wl.get("procedural", False))
+        traffic_src = pmc_traffic_source(p, n, fam, wl.get("procedural", False))
         if flops / bytes_pass < RIDGE:  # HBM-bound fused pass (arithmetic intensity below the ridge)
             roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": kern_ms,
+                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel_ms": kern_ms,
                     "algorithmic_bytes_per_launch": bytes_pass,
                     "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS,
                     "fp64_pipe": mfma_clock_bound(p, n, fam)}
         else:
             roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                    "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
+                    "traffic_source": traffic_src, "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
                     "hbm_gbs_algorithmic": gbs, "fp64_pipe": mfma_clock_bound(p, n, fam, wl.get("procedural", False))}
             # the MFMA instruction stream at the clock the chip holds under the kernel (PMC), against
             # the measured kernel time: how close the kernel is to its clock-limited bound
@@ -554,7 +577,8 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
             "r2": fit.r2, "sse": fit.sse,
             "roofline": {"bound": "hbm", "kernel": st["pass_kernel_name"] + " (LM Gram)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": None, "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass,
+                         "traffic": None, "traffic_source": "none: no PMC pass stored for the LM Gram shape",
+                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass,
                          "note": "1M x 20 = 168 MB per pass: launch- and latency-bound, not a bandwidth test"},
             "breakdown_ms_per_step": {"gram_pass_kernel": kern_ms, "reduce": st["reduce_kernel_ms"] / args.steps,
                                       "solve": st["solve_ms"] / args.steps, "comm": st["comm_ms"] / args.steps},
@@ -572,5 +596,19 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
     return 0
 
 
+def _run() -> int:
+    """main() with a named failure: a rank whose fit fails (e.g. SGLM_ECOMM when a peer rank died
+    and the all-reduce missed its SGLM_COMM_TIMEOUT_S deadline) says which rank and why and exits
+    non-zero at once, without waiting in a collective of the torch group for peers that are gone."""
+    try:
+        return main()
+    except Exception as exc:  # noqa: BLE001  (reported, then a non-zero exit)
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        log(f"[rank {os.environ.get('RANK', '0')}] bench failed: {type(exc).__name__}: {exc}")
+        sys.stderr.flush()
+        os._exit(1)
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(_run())

@@ -92,6 +92,11 @@ class SGLMError(RuntimeError):
         self.code = code
 
 
+class CommError(SGLMError):
+    """SGLM_ECOMM: the all-reduce failed -- RCCL or caller error, or no completion within
+    SGLM_COMM_TIMEOUT_S (a peer rank died or stalled); the message names the rank."""
+
+
 class IllegalArgumentException(ValueError):
     """The reference's require(...) failures (java.lang.IllegalArgumentException)."""
 
@@ -198,6 +203,8 @@ def check(rc: int, what: str = "") -> None:
         raise IllegalArgumentException(msg)
     if rc == SGLM_ESINGULAR:
         raise MatrixSingularException(msg)
+    if rc == SGLM_ECOMM:
+        raise CommError(rc, f"{what}: {msg}" if what else msg)
     raise SGLMError(rc, f"{what}: {msg}" if what else msg)
 
 

@@ -12,6 +12,7 @@
 #include "driver.hpp"
 
 #include <chrono>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -240,8 +241,10 @@ int lm_drive(Backend& be, sglm_prelm* out) {
   be.solve_ms += now_ms() - t0;
   be.solve_path = solver->path();
   const double ymean = ysum / nrow;  // LM.scala:167-168
-  // the device's residual statistics stand only if its solve was this one, bit for bit
-  if (!dev || std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
+  // the device's residual statistics stand only if its solve was this one, bit for bit; a device
+  // Cholesky that failed a pivot returns NaN coefficients (its statistics are never used)
+  const bool dev_failed = dev && std::any_of(dev_coefs.begin(), dev_coefs.end(), [](double v) { return std::isnan(v); });
+  if (!dev || dev_failed || std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
     rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
     if (rc) return rc;
     if (dev) be.lm_device_reruns += 1;

@@ -66,6 +66,189 @@ double now_ms() {
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// ---- bounded waits on the per-iteration all-reduce (utils.scala:110-126's treeReduce seam) ----
+// A rank that dies or stalls must not hang the others until an outside time limit: every wait on
+// a collective has a deadline, SGLM_COMM_TIMEOUT_S seconds (default 300; 0 = unbounded), read when
+// the communicator is set.  On expiry (or an asynchronous RCCL error) the call returns SGLM_ECOMM
+// naming the rank and what it waited for, and the communicator is unusable from then on.
+double comm_timeout_ms_env() {
+  const char* e = std::getenv("SGLM_COMM_TIMEOUT_S");
+  if (!e || !*e) return 300e3;
+  const double s = std::atof(e);
+  return s > 0.0 ? s * 1e3 : 0.0;
+}
+
+std::string rank_str(int rank) { return rank >= 0 ? "rank " + std::to_string(rank) : "this rank"; }
+
+// Wait for the streams whose last work is a collective over `comms` (the engine's RCCL
+// communicator, or a multi-device handle's ncclCommInitAll group): poll hipStreamQuery and every
+// communicator's asynchronous error until the streams drain or the deadline passes.  On a remote
+// error or expiry the communicators are aborted (ncclCommAbort makes their kernels exit) and
+// nulled, and SGLM_ECOMM is returned -- never a silent hang.
+int wait_collective(const std::vector<hipStream_t>& sts, std::vector<ncclComm_t*> comms, double timeout_ms,
+                    int rank, const char* what) {
+  const double t0 = now_ms();
+  std::vector<char> done(sts.size(), 0);
+  size_t left = sts.size();
+  auto abort_all = [&](const std::string& why) {
+    for (ncclComm_t* c : comms)
+      if (*c) {
+        (void)ncclCommAbort(*c);
+        *c = nullptr;
+      }
+    set_error(why);
+    return SGLM_ECOMM;
+  };
+  for (uint64_t it = 0; left > 0; ++it) {
+    for (size_t i = 0; i < sts.size(); ++i) {
+      if (done[i]) continue;
+      const hipError_t e = hipStreamQuery(sts[i]);
+      if (e == hipSuccess) {
+        done[i] = 1;
+        --left;
+      } else if (e != hipErrorNotReady) {
+        set_error(hip_msg(e, "hipStreamQuery (wait on the all-reduce)"));
+        return SGLM_EHIP;
+      }
+    }
+    if (left == 0) break;
+    if ((it & 255) == 255) {
+      for (ncclComm_t* c : comms) {
+        ncclResult_t ae = ncclSuccess;
+        if (*c && ncclCommGetAsyncError(*c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+          return abort_all(std::string("RCCL asynchronous error on ") + rank_str(rank) + " during " + what + ": " +
+                           ncclGetErrorString(ae) + "; communicator aborted");
+      }
+      if (timeout_ms > 0.0 && now_ms() - t0 > timeout_ms)
+        return abort_all(rank_str(rank) + ": " + what + " did not complete within SGLM_COMM_TIMEOUT_S = " +
+                         std::to_string(timeout_ms * 1e-3) + " s (a peer rank died, stalled or never joined); "
+                         "communicator aborted");
+    }
+    std::this_thread::yield();
+  }
+  return SGLM_OK;
+}
+
+// Caller-supplied all-reduce callbacks (sglm_set_comm, sglm_fit_*_external) run on a communicator
+// thread owned by the handle -- one thread for the handle's life, with the handle's device
+// current -- while the calling thread waits with the deadline.  A callback that never returns is
+// abandoned (its thread detached with its own copy of a host buffer) and the handle's communicator
+// is marked broken.  sglm_local_allreduce is bounded by itself and runs inline.
+class CallbackRunner {
+ public:
+  explicit CallbackRunner(int device = -1) : device_(device) {}
+  ~CallbackRunner() {
+    if (!st_) return;
+    {
+      std::lock_guard<std::mutex> lk(st_->mu);
+      st_->stop = true;
+    }
+    st_->cv.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  CallbackRunner(const CallbackRunner&) = delete;
+  CallbackRunner& operator=(const CallbackRunner&) = delete;
+
+  bool broken() const { return !broken_msg_.empty(); }
+  // a timed-out device-buffer callback may still write its buffer: the owner must not free it
+  bool leaked_device_buffer() const { return leaked_dev_; }
+  void reset() {  // a new communicator
+    broken_msg_.clear();
+    leaked_dev_ = false;
+  }
+  int call(sglm_allreduce_fn fn, void* ctx, double* buf, int64_t count, void* stream, int on_device, double timeout_ms,
+           int rank) {
+    if (broken()) {
+      set_error(broken_msg_);
+      return SGLM_ECOMM;
+    }
+    if (timeout_ms <= 0.0 || fn == &sglm_local_allreduce) {
+      if (fn(ctx, buf, count, stream, on_device) != 0) {
+        set_error(fn == &sglm_local_allreduce
+                      ? "in-process all-reduce failed on " + rank_str(rank) +
+                            " (ranks passed different lengths, or a rank did not arrive within SGLM_COMM_TIMEOUT_S)"
+                      : "caller all-reduce failed on " + rank_str(rank));
+        return SGLM_ECOMM;
+      }
+      return SGLM_OK;
+    }
+    start();
+    std::unique_lock<std::mutex> lk(st_->mu);
+    st_->fn = fn;
+    st_->ctx = ctx;
+    st_->count = count;
+    st_->stream = stream;
+    st_->on_device = on_device;
+    if (on_device) {
+      st_->buf = buf;
+    } else {
+      st_->host.assign(buf, buf + count);
+      st_->buf = st_->host.data();
+    }
+    st_->done = false;
+    st_->has_job = true;
+    st_->cv.notify_all();
+    const bool ok = st_->cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms), [&] { return st_->done; });
+    if (!ok) {
+      lk.unlock();
+      broken_msg_ = rank_str(rank) + ": the caller all-reduce did not return within SGLM_COMM_TIMEOUT_S = " +
+                    std::to_string(timeout_ms * 1e-3) + " s (a peer rank died, stalled or never joined); the "
+                    "communicator is broken -- set a new one";
+      leaked_dev_ = on_device != 0;
+      th_.detach();  // the thread keeps its state (and the host copy) alive by itself
+      st_.reset();
+      set_error(broken_msg_);
+      return SGLM_ECOMM;
+    }
+    if (!on_device) std::memcpy(buf, st_->host.data(), sizeof(double) * (size_t)count);
+    if (st_->rc != 0) {
+      set_error("caller all-reduce failed on " + rank_str(rank));
+      return SGLM_ECOMM;
+    }
+    return SGLM_OK;
+  }
+
+ private:
+  struct State {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool has_job = false, done = false, stop = false;
+    sglm_allreduce_fn fn = nullptr;
+    void* ctx = nullptr;
+    double* buf = nullptr;
+    int64_t count = 0;
+    void* stream = nullptr;
+    int on_device = 0, rc = 0;
+    std::vector<double> host;
+  };
+  void start() {
+    if (st_) return;
+    st_ = std::make_shared<State>();
+    std::shared_ptr<State> s = st_;
+    const int dev = device_;
+    th_ = std::thread([s, dev] {
+      if (dev >= 0) (void)hipSetDevice(dev);
+      std::unique_lock<std::mutex> lk(s->mu);
+      for (;;) {
+        s->cv.wait(lk, [&] { return s->has_job || s->stop; });
+        if (s->stop) return;
+        s->has_job = false;
+        lk.unlock();
+        const int rc = s->fn(s->ctx, s->buf, s->count, s->stream, s->on_device);
+        lk.lock();
+        s->rc = rc;
+        s->done = true;
+        s->cv.notify_all();
+      }
+    });
+  }
+  int device_;
+  std::shared_ptr<State> st_;
+  std::thread th_;
+  std::string broken_msg_;
+  bool leaked_dev_ = false;
+};
+
 struct Comm {
   int kind = 0;  // 0 none, 1 callback, 2 rccl
   sglm_allreduce_fn fn = nullptr;
@@ -75,6 +258,7 @@ struct Comm {
   int nranks = 1;
   int rank = -1;  // this handle's rank (RCCL, the in-process communicator, sglm_set_comm_rank); -1 unknown
   double ms = 0.0;
+  double timeout_ms = 300e3;  // SGLM_COMM_TIMEOUT_S when the communicator was set (0: unbounded)
 };
 
 // Cross-rank sums of the NS scalars (deviance, Pearson, loglik ingredients, ...) in rank order
@@ -271,12 +455,14 @@ struct sglm_engine : public Backend {
   std::vector<sglm_engine*> subs;
   std::vector<int64_t> sub_lo;       // first global row of each shard
   std::vector<ncclComm_t> gcomms;    // ncclCommInitAll over distinct devices (else host sums)
+  bool group_aborted = false;        // a group all-reduce missed its deadline (wait_collective)
   int64_t g_n = 0;                   // group: total rows
   bool group() const { return !subs.empty(); }
 
   ~sglm_engine() override {
     for (sglm_engine* s : subs) delete s;
-    for (ncclComm_t c : gcomms) (void)ncclCommDestroy(c);
+    for (ncclComm_t c : gcomms)
+      if (c) (void)ncclCommDestroy(c);
     subs.clear();
     gcomms.clear();
     release();
@@ -288,6 +474,7 @@ struct sglm_engine : public Backend {
       *ptr = nullptr;
     }
     n = p = n_pad = nblocks = 0;
+    lm_last_pass_ms = -1.0;  // a new shard: the next device LM fit is timed
     rows_loaded = 0;
     written.clear();
     consts_family = -1;
@@ -352,16 +539,36 @@ struct sglm_engine : public Backend {
   // after_pass: dbuf is the pass just enqueued (ev2 marks its end on st); the RCCL time is then
   // ev2 -> evc on the device (this rank's wait for the others included), not the host wall time
   // of a synchronize that would also cover the pass kernels.
+  std::unique_ptr<CallbackRunner> cbr;  // caller callbacks with a deadline (CallbackRunner)
+  CallbackRunner& runner() {
+    if (!cbr) cbr.reset(new CallbackRunner(device));
+    return *cbr;
+  }
+  // a caller callback abandoned at its deadline may still write the device buffer it was given:
+  // those buffers are leaked, never freed under it
+  void leak_comm_buffers() {
+    dred = dsmall = nullptr;
+    red_cap = dsmall_cap = 0;
+  }
+  int call_comm(double* buf, int64_t count, int on_device) {
+    const int rc = runner().call(comm.fn, comm.ctx, buf, count, (void*)st, on_device, comm.timeout_ms, comm.rank);
+    if (rc && runner().leaked_device_buffer()) leak_comm_buffers();
+    return rc;
+  }
   int allreduce_device(double* dbuf, int64_t count, bool after_pass = false) {
     if (comm.kind == 2) {
+      if (!comm.nccl) {
+        set_error(rank_str(comm.rank) + ": the RCCL communicator was aborted by an earlier failure; set a new one");
+        return SGLM_ECOMM;
+      }
       const double t0 = now_ms();
       ncclResult_t r = ncclAllReduce(dbuf, dbuf, (size_t)count, ncclFloat64, ncclSum, comm.nccl, st);
       if (r != ncclSuccess) {
-        set_error(std::string("RCCL ncclAllReduce: ") + ncclGetErrorString(r));
+        set_error(std::string("RCCL ncclAllReduce on ") + rank_str(comm.rank) + ": " + ncclGetErrorString(r));
         return SGLM_ECOMM;
       }
       if (after_pass) HIPCHK(hipEventRecord(evc, st));
-      HIPCHK(hipStreamSynchronize(st));
+      if (int rc = wait_collective({st}, {&comm.nccl}, comm.timeout_ms, comm.rank, "ncclAllReduce")) return rc;
       if (after_pass) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, ev2, evc));
@@ -372,10 +579,7 @@ struct sglm_engine : public Backend {
     } else if (comm.kind == 1 && comm.on_device) {
       HIPCHK(hipStreamSynchronize(st));
       const double t0 = now_ms();
-      if (comm.fn(comm.ctx, dbuf, count, (void*)st, 1) != 0) {
-        set_error("caller all-reduce failed");
-        return SGLM_ECOMM;
-      }
+      if (int rc = call_comm(dbuf, count, 1)) return rc;
       comm.ms += now_ms() - t0;
     }
     return SGLM_OK;
@@ -383,10 +587,7 @@ struct sglm_engine : public Backend {
   int allreduce_host(double* hbuf, int64_t count) {
     if (comm.kind == 1 && !comm.on_device) {
       const double t0 = now_ms();
-      if (comm.fn(comm.ctx, hbuf, count, (void*)st, 0) != 0) {
-        set_error("caller all-reduce failed");
-        return SGLM_ECOMM;
-      }
+      if (int rc = call_comm(hbuf, count, 0)) return rc;
       comm.ms += now_ms() - t0;
     }
     return SGLM_OK;
@@ -1039,10 +1240,12 @@ struct sglm_engine : public Backend {
   }
   // An untimed pass (enqueue_pass timed = false: LM.fit on the device, see lm_device) counts the
   // kernel times of the last timed one.
+  // (LM fits keep their own last timing: another pass kind in between must not be booked as LM time)
+  double lm_last_pass_ms = -1.0, lm_last_reduce_ms = 0.0;
   void pass_untimed() {
     passes += 1;
-    pass_ms += last_pass_ms;
-    reduce_ms += last_reduce_ms;
+    pass_ms += lm_last_pass_ms;
+    reduce_ms += lm_last_reduce_ms;
   }
 
   // H2D beta, the pass kernels and the fixed-order partial reduction into dred -- all
@@ -1255,6 +1458,10 @@ struct sglm_engine : public Backend {
     const int64_t pp = subs[0]->p, plen = packed_len(pp), sc = tri_count(pp) + pp;
     const int D = (int)subs.size();
     const int64_t len = plen + (int64_t)NS * D;
+    if (group_aborted) {
+      set_error("the multi-device handle's RCCL group was aborted by an earlier failure; create a new handle");
+      return SGLM_ECOMM;
+    }
     for (sglm_engine* s : subs) {
       HIPCHK(hipSetDevice(s->device));
       if (int rc = s->ensure_red_len(len)) return rc;
@@ -1281,10 +1488,21 @@ struct sglm_engine : public Backend {
       sglm_engine* s0 = subs[0];
       HIPCHK(hipSetDevice(s0->device));
       HIPCHK(hipMemcpyAsync(s0->hred, s0->dred, sizeof(double) * len, hipMemcpyDeviceToHost, s0->st));
+      {  // every shard's stream drains, or the group is aborted at the deadline (wait_collective)
+        std::vector<hipStream_t> sts;
+        std::vector<ncclComm_t*> cs;
+        for (int d = 0; d < D; ++d) {
+          sts.push_back(subs[d]->st);
+          cs.push_back(&gcomms[d]);
+        }
+        if (int rc = wait_collective(sts, cs, comm.timeout_ms, -1, "the multi-device ncclAllReduce group")) {
+          group_aborted = true;  // the handle's communicators are gone: every later pass fails
+          return rc;
+        }
+      }
       double cms = -1.0;
       for (sglm_engine* s : subs) {
         HIPCHK(hipSetDevice(s->device));
-        HIPCHK(hipStreamSynchronize(s->st));
         if (int rc = s->pass_timing()) return rc;
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, s->ev2, s->evc));
@@ -1341,7 +1559,7 @@ struct sglm_engine : public Backend {
     // a kernel that carries a completion event ends ~4.5 us later than one that does not (its
     // end-of-kernel signal; measured on the configs[0] timeline): LM fits time their Gram pass on
     // every 16th fit and count that time for the others (pass_untimed)
-    const bool timed = (lm_device_fits % 16) == 0;
+    const bool timed = (lm_device_fits % 16) == 0 || lm_last_pass_ms < 0.0;
     if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, timed)) return rc;
     double* aux = dsmall + NS;  // {ybar, leave-Cholesky flag}
     double* dstat = dred + plen;
@@ -1369,6 +1587,8 @@ struct sglm_engine : public Backend {
     HIPCHK(hipStreamSynchronize(st));  // (a spin on hipStreamQuery measured slower: 0.124 against 0.115 ms)
     if (timed) {
       if (int rc = pass_timing()) return rc;
+      lm_last_pass_ms = last_pass_ms;
+      lm_last_reduce_ms = last_reduce_ms;
     } else {
       pass_untimed();
     }
@@ -1638,15 +1858,13 @@ struct ExternalBackend : public Backend {
   void* ctx;
   int nranks = 1;
   int rank = -1;  // known for the in-process communicator: scalars then summed in rank blocks
+  double timeout_ms = comm_timeout_ms_env();
+  CallbackRunner runner;  // the callback on a communicator thread, waited for with the deadline
   ExternalBackend(const sglm_backend* b, sglm_allreduce_fn f, void* c) : be(b), fn(f), ctx(c), rank(known_rank(f, c)) {}
   int64_t ncols() const override { return be->p; }
   int npart() const override { return nranks; }
   int reduce_raw(double* buf, int64_t count) {
-    if (fn && fn(ctx, buf, count, nullptr, 0) != 0) {
-      set_error("caller all-reduce failed");
-      return SGLM_ECOMM;
-    }
-    return SGLM_OK;
+    return fn ? runner.call(fn, ctx, buf, count, nullptr, 0, timeout_ms, rank) : SGLM_OK;
   }
   // buf[0, count): the last nsc entries are scalar sums -- through rank blocks when the rank is known
   int reduce(double* buf, int64_t count, int64_t nsc) {
@@ -1788,6 +2006,7 @@ int sglm_create_multi(const int* devs, int ndev, sglm_engine** out) {
   bool distinct = true;
   for (int a = 0; a < ndev; ++a)
     for (int b = 0; b < a; ++b) distinct = distinct && devs[a] != devs[b];
+  g->comm.timeout_ms = comm_timeout_ms_env();  // the group all-reduce's deadline (wait_collective)
   if (distinct) {  // one communicator per device, one process (ncclCommInitAll)
     g->gcomms.assign((size_t)ndev, nullptr);
     ncclResult_t r = ncclCommInitAll(g->gcomms.data(), ndev, devs);
@@ -2001,21 +2220,20 @@ int sglm_set_comm(sglm_engine* h, sglm_allreduce_fn fn, void* ctx, int on_device
   h->comm.on_device = on_device;
   h->comm.nranks = 1;
   h->comm.rank = known_rank(fn, ctx);
+  h->comm.timeout_ms = comm_timeout_ms_env();
+  if (h->cbr) h->cbr->reset();
   if (fn) {  // count the ranks joined by the caller's communicator
     double one[1] = {1.0};
     if (on_device) {
       HIPCHK(hipSetDevice(h->device));
       if (int rc = h->ensure_small(64)) return rc;
       HIPCHK(hipMemcpy(h->dsmall, one, sizeof(double), hipMemcpyHostToDevice));
-      if (fn(ctx, h->dsmall, 1, (void*)h->st, 1) != 0) {
-        set_error("caller all-reduce failed");
-        return SGLM_ECOMM;
-      }
+      HIPCHK(hipStreamSynchronize(h->st));
+      if (int rc = h->call_comm(h->dsmall, 1, 1)) return rc;
       HIPCHK(hipStreamSynchronize(h->st));
       HIPCHK(hipMemcpy(one, h->dsmall, sizeof(double), hipMemcpyDeviceToHost));
-    } else if (fn(ctx, one, 1, (void*)h->st, 0) != 0) {
-      set_error("caller all-reduce failed");
-      return SGLM_ECOMM;
+    } else if (int rc = h->call_comm(one, 1, 0)) {
+      return rc;
     }
     h->comm.nranks = (int)std::lround(one[0]);
   }
@@ -2054,6 +2272,7 @@ int sglm_set_comm_rccl(sglm_engine* h, int nranks, int rank, const void* unique_
   h->comm.kind = 2;
   h->comm.nranks = nranks;
   h->comm.rank = rank;
+  h->comm.timeout_ms = comm_timeout_ms_env();
   if (int rc = h->ensure_small(64)) return rc;
   return SGLM_OK;
 }
@@ -2061,21 +2280,26 @@ int sglm_set_comm_rccl(sglm_engine* h, int nranks, int rank, const void* unique_
 int sglm_set_comm_rank(sglm_engine* h, int rank) {
   if (int rc = check_handle(h)) return rc;
   if (int rc = no_group(h, "sglm_set_comm_rank")) return rc;
-  if (h->comm.kind == 0 || rank < 0 || rank >= h->comm.nranks) {
+  if (h->comm.kind == 0) {  // no communicator: no other rank to wait for
     set_error("requirement failed: a communicator joined first (sglm_set_comm), 0 <= rank < its rank count");
     return SGLM_EINVAL;
   }
   // Collective: with a rank the scalars travel in per-rank blocks, which lengthens every later
   // all-reduce, so every rank must opt in -- with distinct ranks -- or the ranks would post
-  // collectives of different sizes.  One plain all-reduce of (1, r, r^2, r^3) checks both.
+  // collectives of different sizes.  Every rank joins one plain all-reduce of [bad | one-hot of
+  // its rank], a rank whose own check fails with bad = 1 (never returning before the collective,
+  // which would leave the others waiting in it): the ranks are valid and distinct iff bad sums to
+  // 0 and every one-hot slot to exactly 1.
   HIPCHK(hipSetDevice(h->device));
   h->comm.rank = -1;
-  const double r = rank;
-  double chk[4] = {1.0, r, r * r, r * r * r};
-  if (int rc = h->allreduce_small(chk, 4)) return rc;
-  const double n = h->comm.nranks;
-  const bool ok = chk[0] == n && chk[1] == n * (n - 1) / 2 && chk[2] == (n - 1) * n * (2 * n - 1) / 6 &&
-                  chk[3] == (n * (n - 1) / 2) * (n * (n - 1) / 2);
+  const int nr = h->comm.nranks;
+  const bool local_ok = rank >= 0 && rank < nr;
+  std::vector<double> chk((size_t)nr + 1, 0.0);
+  chk[0] = local_ok ? 0.0 : 1.0;
+  if (local_ok) chk[(size_t)rank + 1] = 1.0;
+  if (int rc = h->allreduce_small(chk.data(), (int64_t)chk.size())) return rc;
+  bool ok = chk[0] == 0.0;
+  for (int k = 0; k < nr; ++k) ok = ok && chk[(size_t)k + 1] == 1.0;
   if (!ok) {
     set_error("requirement failed: sglm_set_comm_rank must be called by every rank of the communicator, each with "
               "its own distinct rank in [0, " + std::to_string(h->comm.nranks) + ")");
@@ -2371,7 +2595,20 @@ int sglm_local_allreduce(void* ctx, double* buf, int64_t count, void* stream, in
     ++c->generation;
     c->cv.notify_all();
   } else {
-    c->cv.wait(lk, [&] { return c->generation != gen; });
+    // bounded (SGLM_COMM_TIMEOUT_S): a rank that never arrives fails the round for everyone
+    // instead of leaving the others blocked; the one timing out withdraws its buffer
+    const double tmo = comm_timeout_ms_env();
+    auto arrived = [&] { return c->generation != gen; };
+    if (tmo > 0.0) {
+      if (!c->cv.wait_for(lk, std::chrono::duration<double, std::milli>(tmo), arrived)) {
+        c->bufs[(size_t)rk->rank] = nullptr;
+        --c->arrived;
+        c->failed = true;
+        return 1;
+      }
+    } else {
+      c->cv.wait(lk, arrived);
+    }
   }
   return c->result ? 1 : 0;
 }

@@ -220,8 +220,9 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 // the values past it are not used).  Earlier forms -- one wave in LDS, left-looking, 37 us at p = 20;
 // right-looking 26 us; four waves over LDS with a barrier a step 19 us -- were bound by the per-step
 // LDS round trips and barriers on the 20-pivot chain.
-// Out: beta[p]; aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where the host would leave
-// Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO: solve.cpp chol_pivot_ratio).
+// Out: beta[p] (NaN when a pivot failed); aux[0] = sum y / rows (LM.scala:167-168), aux[1] = 1 where
+// the host would leave Cholesky (a non-positive pivot, or the pivot ratio below LU_SWITCH_RATIO:
+// solve.cpp chol_pivot_ratio).
 __device__ __forceinline__ double lane_bcast(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
@@ -280,6 +281,8 @@ __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ 
       if (i == r) tb = xr;
     }
     if (row) beta[i] = tb;
+  } else if (row) {
+    beta[i] = __builtin_nan("");  // no coefficients: the host sees NaN and runs its own residual pass
   }
   double r = (row && dgi > 0.0) ? (diag * diag) / dgi : 1.0;  // chol_pivot_ratio: min over j (exact, any order)
   for (int o = 1; o < 64; o <<= 1) r = fmin(r, __shfl_xor(r, o));
@@ -455,8 +458,9 @@ hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double*
 
 hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st, const double* src,
                                double* host, int64_t ncopy) {
-  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(32 * NS), 0, st, part, nparts, out, src, host, ncopy,
-                     (int64_t)(out - src));
+  // out's offset inside src: only meaningful (and only computed) when the result buffer is copied
+  const int64_t out_off = (src && host) ? (int64_t)(out - src) : 0;
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(32 * NS), 0, st, part, nparts, out, src, host, ncopy, out_off);
   return hipGetLastError();
 }
 

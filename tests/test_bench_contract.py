@@ -43,6 +43,25 @@ def test_pmc_traffic_lookup():
     assert bench.pmc_traffic(333, 10, "binomial") is None
 
 
+def test_roofline_traffic_is_the_stored_pmc_scaled_and_says_so():
+    # the line's `traffic` is the stored PMC bytes/row x the launch's rows, and
+    # `traffic_source` names the table entry and its profiling size
+    tab = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for name, wl in bench.WORKLOADS.items():
+        if wl.get("lm"):
+            continue
+        n = wl["rows"] or wl["strong_rows"]
+        proc = wl.get("procedural", False)
+        key = f"{wl['family']}:{wl['p']}" + (":proc" if proc else "")
+        t = bench.pmc_traffic(wl["p"], n, wl["family"], proc)
+        src = bench.pmc_traffic_source(wl["p"], n, wl["family"], proc)
+        assert key in tab, name
+        assert t == tab[key]["bytes_per_row"] * n, name
+        assert src.startswith("stored PMC, profiles/pmc_traffic.json") and repr(key) in src, name
+        assert str(tab[key]["measured_rows"]) in src and f"x {n} rows" in src, name
+    assert bench.pmc_traffic_source(333, 10, "binomial") is None
+
+
 def test_every_baseline_config_has_a_workload():
     cfgs = json.load(open(os.path.join(ROOT, "BASELINE.json")))["configs"]
     assert {wl["cfg"] for wl in bench.WORKLOADS.values()} == set(range(len(cfgs)))

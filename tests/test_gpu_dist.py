@@ -97,3 +97,64 @@ def test_sharded_fit_equals_oracle(mode, world):
         assert int(s[4]) == ref.iter and s[5] == 40_000 and int(s[6]) == world
         assert rel(coefs, ref.coefs) < 1e-9 and rel(se, ref.stderr) < 1e-9
         assert rel(s[:4], [ref.deviance, ref.null_deviance, ref.pearson, ref.loglik]) < 1e-9
+
+
+def _fail_worker(rank, world, port, case, q):
+    """Failure modes of the rank protocol: `badrank` -- rank 1 passes an out-of-range rank to
+    sglm_set_comm_rank (every rank must still join the check's all-reduce and all of them
+    get SGLM_EINVAL); `deadpeer` -- rank 1 exits before the fit's first collective, rank 0 must get
+    SGLM_ECOMM within SGLM_COMM_TIMEOUT_S instead of hanging."""
+    sys.path.insert(0, ROOT)
+    os.environ["SGLM_COMM_TIMEOUT_S"] = "10"
+    import time
+    import torch
+    import torch.distributed as dist
+    from sparkglm_amd import Engine, synth
+    from sparkglm_amd import distributed as D
+    from sparkglm_amd._lib import CommError, IllegalArgumentException
+    X, y, off, pr = synth.generate(2, 1000 * rank, 1000, 8, 5)
+    eng = Engine(0)
+    eng.set_data(X, y, offset=off, prior=pr)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if case == "badrank":
+        try:
+            eng.set_comm(D.torch_allreduce(), on_device=True, rank=5 if rank == 1 else rank)
+            q.put((rank, "no error"))
+        except IllegalArgumentException as exc:
+            q.put((rank, "einval:" + str(exc)))
+        dist.barrier()
+        eng.close()
+        dist.destroy_process_group()
+        return
+    eng.set_comm(D.torch_allreduce(), on_device=True, rank=rank)
+    if rank == 1:
+        q.put((rank, "exited"))
+        os._exit(0)  # dies before the fit's first collective
+    t0 = time.perf_counter()
+    try:
+        eng.fit_glm("poisson", "log", init="multiple")
+        q.put((rank, "no error"))
+    except CommError as exc:
+        q.put((rank, f"ecomm:{time.perf_counter() - t0:.1f}:{exc}"))
+    os._exit(0)  # the gloo group lost a member: skip its teardown
+
+
+@pytest.mark.parametrize("case", ["badrank", "deadpeer"])
+def test_rank_failures_end_with_an_error_not_a_hang(case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    if case == "badrank":
+        for r in (0, 1):
+            assert res[r].startswith("einval:") and "distinct rank" in res[r], res[r]
+    else:
+        assert res[1] == "exited"
+        assert res[0].startswith("ecomm:"), res[0]
+        assert float(res[0].split(":")[1]) < 60.0, res[0]

@@ -84,3 +84,37 @@ def test_ill_conditioned_falls_back_to_the_host_lu():
     _same(res[True][0], res[False][0])
     r = po.fit_lm(X, y)
     assert rel(res[True][0].sse, r["sse"]) < 1e-9
+
+
+def _fit_or_exc(e):
+    try:
+        return e.fit_lm()
+    except Exception as exc:  # noqa: BLE001
+        return type(exc)
+
+
+@pytest.mark.parametrize("kind", ["zero_column", "duplicate_column"])
+def test_rank_deficient_design_takes_the_host_path(kind):
+    # a pivot that is not positive makes lm_chol_kernel return NaN coefficients, and
+    # lm_drive then never uses the device's residual statistics -- the fit (or its
+    # MatrixSingularException) is the two-round-trip path's, bit for bit
+    rng = np.random.default_rng(11)
+    n = 50_000
+    X = np.asfortranarray(np.c_[np.ones(n), rng.uniform(-1, 1, (n, 4))])
+    if kind == "zero_column":
+        X[:, 3] = 0.0  # X'X has an exactly zero diagonal: the device pivot is 0
+    else:
+        X[:, 3] = X[:, 1]  # exactly rank deficient
+    y = X[:, :3] @ np.array([1.0, 0.5, -0.25]) + rng.uniform(-1, 1, n)
+    out = {}
+    for device in (True, False):
+        with _engine(device) as e:
+            e.set_data(X, y)
+            out[device] = (_fit_or_exc(e), e.stats())
+    fd, fh = out[True][0], out[False][0]
+    if isinstance(fd, type):
+        assert fd is fh, (fd, fh)
+    else:
+        assert not isinstance(fh, type)
+        _same(fd, fh)
+        assert out[True][1]["lm_device_reruns"] == 1  # the host's coefficients, the host's residual pass

@@ -1,0 +1,55 @@
+#!/bin/bash
+# Round-5 GPU session: stages as in r04_gpu.sh (test, bench, benchw, ab, ...).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+STAGES=${1:-cap,test,bench}
+if [[ ,$STAGES, == *,cap,* ]]; then
+  timeout -k 10 300 python -u tools/gram_split_capture.py > gpurun_out/cap.log 2>&1 || { echo "capture failed"; tail -20 gpurun_out/cap.log; exit 1; }
+  tail -3 gpurun_out/cap.log
+fi
+if [[ ,$STAGES, == *,test,* ]]; then
+  timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -rA --timeout 300 --timeout-method thread -W ignore > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+  cat gpurun_out/smoke.log
+fi
+if [[ ,$STAGES, == *,ab,* ]]; then  # same-box A/B: the round-3 library (lib_ab/head) against the tree
+  export AB_LIBS=sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so AB_REPS=3
+  AN=200000000 AP=32 AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p32.log 2>&1 || { echo "ab p32 failed"; tail gpurun_out/ab_p32.log; exit 1; }
+  AN=125000000 AP=64 AK=2 AF=poisson AL=log timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p64.log 2>&1 || { echo "ab p64 failed"; tail gpurun_out/ab_p64.log; exit 1; }
+  cat gpurun_out/ab_p32.log gpurun_out/ab_p64.log
+fi
+if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default head, tree) at p = 80 / 96 / 112 / 128 / 240
+  export AB_LIBS=${AB_MID_LIBS:-sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=2
+  for pn in ${AB_MID_P:-80:37500000 96:31250000 112:26785714 128:23437500 240:10000000}; do
+    AN=${pn#*:} AP=${pn%:*} AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py >> gpurun_out/ab_mid.log 2>&1 || { echo "ab mid failed"; tail gpurun_out/ab_mid.log; exit 1; }
+  done
+  cat gpurun_out/ab_mid.log
+fi
+if [[ ,$STAGES, == *,sweep,* ]]; then  # mid-width sweep (tools/midp_sweep.py), then the same under rocprofv3
+  timeout -k 10 400 python tools/midp_sweep.py ${SWEEP_P:-} > gpurun_out/midp_sweep.log 2>&1 || { echo "sweep failed"; tail gpurun_out/midp_sweep.log; exit 1; }
+  cat gpurun_out/midp_sweep.log
+  export TMPDIR=/tmp
+  SWEEP_PASSES=3 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_midp" -o midp --output-format csv -- python tools/midp_sweep.py ${SWEEP_P:-} > gpurun_out/prof_midp.log 2>&1 || { echo "sweep prof failed"; tail gpurun_out/prof_midp.log; exit 1; }
+fi
+if [[ ,$STAGES, == *,benchw,* ]]; then  # the other workloads' bench lines (WORKLOADS env: space-separated)
+  for w in ${WORKLOADS:-poisson64}; do
+    timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-load > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { echo "bench $w failed"; tail -20 gpurun_out/bench_$w.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/bench_$w.json')); r=d['roofline']; print('$w', d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], d['iters_to_converge'])"
+  done
+fi
+if [[ ,$STAGES, == *,lm,* ]]; then  # configs[0] host overhead: wall per fit, then the kernel / copy timeline
+  timeout -k 10 300 python tools/lm_timeline.py 300 > gpurun_out/lm_timeline.log 2>&1 || { echo "lm timeline failed"; tail gpurun_out/lm_timeline.log; exit 1; }
+  cat gpurun_out/lm_timeline.log
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_lm" -o lm --output-format csv -- python tools/lm_timeline.py 100 > gpurun_out/prof_lm.log 2>&1 || { echo "lm prof failed"; tail gpurun_out/prof_lm.log; exit 1; }
+fi
+if [[ ,$STAGES, == *,rehearse8,* ]]; then  # 8 ranks sharing this GPU over gloo (the 8-GPU launch path)
+  timeout -k 10 900 python bench.py --gpus 8 --rows 10000000 --steps 3 --warmup 1 --no-load > gpurun_out/bench_gpus8.json 2> gpurun_out/bench_gpus8.err || { echo "rehearsal failed"; tail -20 gpurun_out/bench_gpus8.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_gpus8.json')); s=d['strong_scaling_1b_logit']; print('gpus8', d['n_gpus'], d['ms_per_step'], d['iters_to_converge'], s['n_gpus'], s['iters_to_converge'], repr(s['deviance']))"
+fi
+if [[ ,$STAGES, == *,bench,* ]]; then
+  timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench.json')); r=d['roofline']; s=d.get('strong_scaling_1b_logit') or {}; print(d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], s.get('ms_per_iter'), s.get('time_to_converge_s'))"
+fi

@@ -110,7 +110,9 @@ enum sglm_pass_kernel {
   SGLM_KERNEL_FUSED_SPLIT = 2, /* irls_pass_r_kernel<P16, fam, link> (K1r, split roles) */
   SGLM_KERNEL_NARROW = 3,      /* irls_narrow_kernel<P16, fam, link, irls, stats>: p <= 64 */
   SGLM_KERNEL_WIDE = 4,        /* wide_rows_kernel + wide_gram_kernel: p > 256 (resident X) */
-  SGLM_KERNEL_WIDE_PROC = 5    /* the same over procedural X (generated chunks or in-kernel) */
+  SGLM_KERNEL_WIDE_PROC = 5,   /* the same over procedural X (generated chunks or in-kernel) */
+  SGLM_KERNEL_NARROW_SPLIT = 6 /* irls_narrow_r_kernel<P16, fam, link, irls, stats>: split-role narrow pass,
+                                  33 <= p <= 64 by default (SGLM_NARROW_SPLIT) */
 };
 
 /* Prediction scale (R's predict(type = "link" | "response")). */
@@ -303,7 +305,8 @@ int sglm_get_stats(sglm_engine *h, sglm_stats *out);
 /* The kernel an engine would run a pass of an n x p shard with (enum sglm_pass_kernel, -1 on bad
  * arguments) and its name into name[namelen] -- the engine's own dispatch rule, for callers and CPU
  * tests.  fused_split: SGLM_FUSED_SPLIT's meaning (1 default threshold, 0 never K1r, N from P16 = N);
- * flags: 1 procedural shard, 2 forced wide path (SGLM_FORCE_WIDE).  No device is touched. */
+ * flags: 1 procedural shard, 2 forced wide path (SGLM_FORCE_WIDE), bits 4..7 SGLM_NARROW_SPLIT + 1 (0: the
+ * default threshold).  No device is touched. */
 int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int family, int link, char *name,
                          int64_t namelen);
 int sglm_reset_stats(sglm_engine *h);

@@ -69,7 +69,8 @@ class Stats(C.Structure):
 
 COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}
 SOLVE_PATHS = {-1: "none", 0: "host-cholesky", 1: "host-lu", 2: "device-cholesky", 3: "device-lu"}
-PASS_KERNELS = {0: "none", 1: "fused", 2: "fused-split", 3: "narrow", 4: "wide", 5: "wide-procedural"}
+PASS_KERNELS = {0: "none", 1: "fused", 2: "fused-split", 3: "narrow", 4: "wide", 5: "wide-procedural",
+                6: "narrow-split"}
 
 
 class GlmDerived(C.Structure):
@@ -181,11 +182,12 @@ def load():
 
 
 def pass_kernel_for(n: int, p: int, family: str = "binomial", link: str = "logit", fused_split: int = 1,
-                    procedural: bool = False, force_wide: bool = False):
-    """(kind, name) of the kernel an engine runs an n x p pass with (sglm_pass_kernel_for; no GPU)."""
+                    procedural: bool = False, force_wide: bool = False, narrow_split=None):
+    """(kind, name) of the kernel an engine runs an n x p pass with (sglm_pass_kernel_for; no GPU).
+    narrow_split: SGLM_NARROW_SPLIT's meaning (None: the default threshold, 0 never, N from P16 = N)."""
     buf = C.create_string_buffer(64)
-    k = load().sglm_pass_kernel_for(int(n), int(p), int(fused_split), (1 if procedural else 0) | (2 if force_wide else 0),
-                                    FAMILIES[family], LINKS[link], buf, 64)
+    flags = (1 if procedural else 0) | (2 if force_wide else 0) | ((0 if narrow_split is None else int(narrow_split) + 1) << 4)
+    k = load().sglm_pass_kernel_for(int(n), int(p), int(fused_split), flags, FAMILIES[family], LINKS[link], buf, 64)
     if k < 0:
         raise IllegalArgumentException(last_error())
     return PASS_KERNELS[k], buf.value.decode()

@@ -309,8 +309,14 @@ void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_
 // ensure_workspace / launch_pass / launch_narrow / the wide path, in one place (the engine labels
 // its passes with it; sglm_pass_kernel_for exposes it for a CPU test of the mapping).
 namespace {
-int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc, int fused_split, int family,
-                       int link, char* name, size_t len) {
+// SGLM_NARROW_SPLIT: narrow shards of P16 >= this many column blocks run the split-role narrow pass
+// (irls_narrow_r_kernel, narrow_r.hip); 0 never.  Default 3: 33 <= p <= 64.
+constexpr int NARROW_SPLIT_DEFAULT = 3;
+bool narrow_uses_split(int P16, int narrow_split, int64_t n_pad) {
+  return narrow_split > 0 && P16 >= narrow_split && narrow_r_ok(P16, n_pad);
+}
+int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc, int fused_split, int narrow_split,
+                       int family, int link, char* name, size_t len) {
   static const char* fam[] = {"binomial", "gaussian", "poisson", "gamma"};
   static const char* lnk[] = {"logit", "probit", "cloglog", "identity", "log", "inverse"};
   const char* f = (family >= 0 && family < 4) ? fam[family] : "?";
@@ -319,6 +325,9 @@ int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc
   if (wide) {
     k = proc ? SGLM_KERNEL_WIDE_PROC : SGLM_KERNEL_WIDE;
     std::snprintf(name, len, "wide_gram_kernel<%s>", proc ? "procedural" : "resident");
+  } else if (narrow && narrow_uses_split(P16, narrow_split, n_pad)) {
+    k = SGLM_KERNEL_NARROW_SPLIT;
+    std::snprintf(name, len, "irls_narrow_r_kernel<%d,%s,%s>", P16, f, l);
   } else if (narrow) {
     k = SGLM_KERNEL_NARROW;
     std::snprintf(name, len, "irls_narrow_kernel<%d,%s,%s>", P16, f, l);
@@ -387,8 +396,10 @@ struct sglm_engine : public Backend {
   bool dev_only = false, allow_spec = true;
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
-  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines
-  bool narrow = false;
+  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; narrow_r: its split-role
+  // form (narrow_r.hip) for P16 >= narrow_split (SGLM_NARROW_SPLIT, 0 never)
+  bool narrow = false, narrow_r = false;
+  int narrow_split = NARROW_SPLIT_DEFAULT;
   // procedural shard (sglm_synth_procedural): X regenerated in the wide kernels, not stored
   ProcX procx{};
   // procedural shards in chunks (setup_proc_chunks): each pass generates C rows of X at a time
@@ -884,11 +895,13 @@ struct sglm_engine : public Backend {
       if (rc) return rc;
     }
     narrow = !wide && p <= 64;
+    narrow_r = false;
     if (narrow) {
       P16 = narrow_variant((int)p);
       stride = narrow_stride(P16);
-      const int64_t want_grid = (int64_t)ncu * narrow_wg_per_cu();
-      const int64_t per_wg = narrow_rows_per_wg(P16);
+      narrow_r = narrow_uses_split(P16, narrow_split, n_pad);
+      const int64_t want_grid = (int64_t)ncu * (narrow_r ? 1 : narrow_wg_per_cu());
+      const int64_t per_wg = narrow_r ? NARROW_R_ROWS : narrow_rows_per_wg(P16);
       const int64_t need = (nblocks * RB + per_wg - 1) / per_wg;
       grid = (int)std::max<int64_t>(1, std::min(need, want_grid));
     } else {
@@ -1424,7 +1437,8 @@ struct sglm_engine : public Backend {
       // a tenth of an LM.fit on configs[0]
       hipEvent_t e0 = timed ? ev0 : nullptr, e1 = timed ? ev1 : nullptr, e2 = timed ? ev2 : nullptr;
       if (nblocks > 0) {
-        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, e0, e1));
+        if (narrow_r) HIPCHK(launch_narrow_r(P16, a, grid, st, e0, e1));
+        else if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, e0, e1));
         else HIPCHK(launch_pass(P16, a, grid, st, e0, e1));
       } else {
         HIPCHK(hipEventRecord(ev0, st));
@@ -1443,7 +1457,7 @@ struct sglm_engine : public Backend {
   // own dispatch decision -- narrow / fused / wide, and K1 against K1r by pass_uses_split with its
   // row limit -- so a roofline line is labelled by what ran, not by a re-derived threshold.
   void note_kernel(int family, int link) {
-    last_kernel = pass_kernel_choice(n_pad, P16, narrow, wide, procx.on != 0, fused_split, family, link,
+    last_kernel = pass_kernel_choice(n_pad, P16, narrow, wide, procx.on != 0, fused_split, narrow_split, family, link,
                                      last_kernel_name, sizeof last_kernel_name);
   }
 
@@ -1977,6 +1991,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
   if (const char* ld = std::getenv("SGLM_LM_DEVICE")) h->allow_lm_device = std::atoi(ld) != 0;
   if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::max(0, std::atoi(fs));
+  if (const char* ns = std::getenv("SGLM_NARROW_SPLIT")) h->narrow_split = std::max(0, std::atoi(ns));
   if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "lu") == 0;
   if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
   *out = h;
@@ -2445,7 +2460,11 @@ int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int f
   const bool proc = (flags & 1) != 0, wide = proc || (flags & 2) || p > 16 * MAX_P16, narrow = !wide && p <= 64;
   const int P16 = wide ? 0 : narrow ? narrow_variant((int)p) : pass_variant((int)p, fused_split, n_pad);
   char buf[64];
-  const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, family, link, buf, sizeof buf);
+  // flags bits 4..7: SGLM_NARROW_SPLIT + 1 (0: the default threshold)
+  const int ns_flag = (flags >> 4) & 15;
+  const int narrow_split = ns_flag == 0 ? NARROW_SPLIT_DEFAULT : ns_flag - 1;
+  const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, narrow_split, family, link, buf,
+                                   sizeof buf);
   if (name && namelen > 0) std::snprintf(name, (size_t)namelen, "%s", buf);
   return k;
 }

@@ -53,3 +53,9 @@ if [[ ,$STAGES, == *,bench,* ]]; then
   timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/bench.json')); r=d['roofline']; s=d.get('strong_scaling_1b_logit') or {}; print(d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], s.get('ms_per_iter'), s.get('time_to_converge_s'))"
 fi
+if [[ ,$STAGES, == *,nr,* ]]; then  # split-role narrow pass: parity against irls_narrow_kernel, then pass times
+  timeout -k 10 300 python -u tools/nr_check.py parity > gpurun_out/nr_parity.log 2>&1 || { echo "nr parity failed"; tail -30 gpurun_out/nr_parity.log; exit 1; }
+  cat gpurun_out/nr_parity.log
+  timeout -k 10 300 python -u tools/nr_check.py timing > gpurun_out/nr_timing.log 2>&1 || { echo "nr timing failed"; tail -30 gpurun_out/nr_timing.log; exit 1; }
+  cat gpurun_out/nr_timing.log
+fi

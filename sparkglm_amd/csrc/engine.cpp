@@ -310,8 +310,8 @@ void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_
 // its passes with it; sglm_pass_kernel_for exposes it for a CPU test of the mapping).
 namespace {
 // SGLM_NARROW_SPLIT: narrow shards of P16 >= this many column blocks run the split-role narrow pass
-// (irls_narrow_r_kernel, narrow_r.hip); 0 never.  Default 3: 33 <= p <= 64.
-constexpr int NARROW_SPLIT_DEFAULT = 3;
+// (irls_narrow_r_kernel, narrow_r.hip); 0 never (the default: measured slower, DESIGN.md 4 K1'r).
+constexpr int NARROW_SPLIT_DEFAULT = 0;
 bool narrow_uses_split(int P16, int narrow_split, int64_t n_pad) {
   return narrow_split > 0 && P16 >= narrow_split && narrow_r_ok(P16, n_pad);
 }

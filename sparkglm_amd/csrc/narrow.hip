@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -341,9 +342,45 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       }
     }
   } else {
-#pragma unroll 1
-  for (int64_t blk = b0; blk < b1; ++blk) {
-    const int buf = (int)((blk - b0) & 1);
+  // p > 32 (NRB = 16): the blocks alternate the two buffers, so the loop takes them in pairs with the
+  // buffer a compile-time constant -- every LDS address is then a per-lane base fixed for the kernel
+  // plus an immediate offset (the compiler had formed the eta reads' swizzled addresses with one
+  // v_add3 per read and block), and the DMA keeps one 64-bit source pointer per column group, advanced
+  // once per block (it had carried two 64-bit adds per group and block).
+  // eta reads: lane (g, rl), column c = LPR u + g at (c >> 4) BSTR + (c & 15) NRB + (rl ^ swz(c)); for
+  // u = 4 j + k the lane part depends on k only, j moves by BSTR (immediate)
+  int eoff[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = LPR * k + g;
+    eoff[k] = (c & 15) * NRB + (rl ^ swz<NRB>(c));
+  }
+  // Gram operand reads: lane (rq, cl) reads row 4 s + rq of column 16 b + cl
+  int goff[NRB / 4];
+#pragma unroll
+  for (int s = 0; s < NRB / 4; ++s) goff[s] = cl * NRB + ((4 * s + rq) ^ fcl);
+  // DMA sources of the next block to stage (blocks are staged in order, b0 + 2 onwards)
+  const double* dsrc[G::NOCT];
+#pragma unroll
+  for (int o = 0; o < G::NOCT; ++o) {
+    const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
+    dsrc[o] = a.X + (b0 + 2) * NRB + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER];
+  }
+  const double* vnext = vsrc + (b0 + 2) * NRB;
+  auto stage_next = [&](auto bufc) {
+    constexpr int BUFI = decltype(bufc)::value;
+    double* dst = wl + BUFI * G::BUF;
+#pragma unroll
+    for (int o = 0; o < G::NOCT; ++o) {
+      __builtin_amdgcn_global_load_lds((const void*)dsrc[o],
+                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, 0);
+      dsrc[o] += NRB;
+    }
+    if (lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, 0);
+    vnext += NRB;
+  };
+  auto block = [&](auto bufc, int64_t blk) {
+    constexpr int BUFI = decltype(bufc)::value;
     // The two waves sharing a SIMD (wv, wv ^ 4) take turns at the higher issue priority every
     // NPRIO blocks: the arbiter otherwise favours the older wave, the younger one falls ~35 %
     // behind on its equal share and finishes alone with no partner to overlap.
@@ -355,17 +392,14 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     if (blk + 1 >= b1) wait_vm<0>();
     else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
     else wait_vm<G::NOCT + 1>();
-    const double* xs = wl + buf * G::BUF;
+    const double* xs = wl + BUFI * G::BUF;
 
     // ---- row stage ----
     double eta = 0.0;
     if (irls) {
       double e4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int u = 0; u < CPL; ++u) {
-        const int c = LPR * u + g;
-        e4[u & 3] += xs[(c >> 4) * G::BSTR + (c & 15) * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
-      }
+      for (int u = 0; u < CPL; ++u) e4[u & 3] += xs[eoff[u & 3] + (u >> 2) * G::BSTR] * bcol[u];
       eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
       if constexpr (LPR == 4) eta = xor16_sum(eta);
       if constexpr (LPR >= 2) eta = xor32_sum(eta);
@@ -384,9 +418,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double off = a.off ? vv[2 * NRB + rl] : 0.0;
         const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
         if constexpr (STATS)
-          pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, P16 <= 2, ylogy);
+          pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true, ylogy);
         else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
-          pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, P16 <= 2,
+          pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                    !IRLS, ylogy);
           if constexpr (INIT_CONST)
             if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
@@ -397,16 +431,15 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     }
 
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
-    if (do_gram) {  // (p > 32 here: p <= 32 takes the row-pair loop above)
+    if (do_gram) {
 #pragma unroll
       for (int s = 0; s < NRB / 4; ++s) {
         const int r = 4 * s + rq;
         const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + NRB + r];
-        const double* base = xs + cl * NRB + (r ^ fcl);
         double xv[P16], av[P16];
 #pragma unroll
         for (int b = 0; b < P16; ++b) {
-          xv[b] = base[G::BSTR * b];
+          xv[b] = xs[goff[s] + G::BSTR * b];
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
@@ -415,7 +448,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     }
     // every LDS read of this buffer has returned before the DMA may overwrite it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+    if (blk + 2 < b1) stage_next(bufc);
+  };
+#pragma unroll 1
+  for (int64_t blk = b0; blk < b1; blk += 2) {
+    block(std::integral_constant<int, 0>{}, blk);
+    if (blk + 1 < b1) block(std::integral_constant<int, 1>{}, blk + 1);
   }
   }  // !PAIR
 

@@ -31,7 +31,8 @@
 // The eta reads (lane = row, one column) cover a 256-byte bank row per half-wave and the MFMA operand
 // reads (lane (rq, cl): row 4k + rq of column 16b + cl) hit 32 distinct 8-byte positions of a bank
 // row per half-wave: both conflict free.  Lane offsets of the DMA sources are 32-bit (column pair
-// part h ld 8 bytes), so the variant needs n_pad < 2^29 rows (narrow_r_ok).
+// part h ld 8 bytes); a shard of n_pad >= 2^29 rows stages each column of a pair by its own half-wave
+// instruction instead (the tall form).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -60,6 +61,7 @@ struct NR {
   static constexpr int NPAIR = NC / 2;                   // DMA wave-instructions of X per block
   static constexpr int PPW = NPAIR / NRW;                // ... per row wave
   static constexpr int VMEM = PPW + 1;                   // vector-memory operations per row wave and block
+  static constexpr int VMEM_TALL = 2 * PPW + 1;          // ... on a tall shard (a column per half-wave instruction)
   static constexpr int OFF_V = XB;                       // y | m | offset | prior  [4][SB]
   static constexpr int OFF_W = XB + 4 * SB;              // w | w*z                 [2][SB]
   static constexpr int OFF_E = XB + 6 * SB;              // eta                     [SB]
@@ -77,7 +79,7 @@ struct NR {
   static_assert(NB >= 3, "ring depth");
   static_assert(LDS * 8 <= 160 * 1024, "LDS budget");
   static_assert((NGW / 2) * PSZ <= NB * PER, "the fold fits the ring");
-  static_assert(VMEM * (NB - 1) < 64, "vmcnt range");
+  static_assert(VMEM_TALL * (NB - 1) < 64, "vmcnt range");
   static_assert(PER % 2 == 0 && XB % 2 == 0, "LDS-DMA destinations 16-byte aligned");
 };
 
@@ -88,16 +90,14 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // wait until the DMA of a block has landed while `later` blocks staged after it may still fly
-template <int VM, int NB>
+template <int VM, int NB, int L = NB - 1>
 __device__ __forceinline__ void wait_landed(int later) {
-  if (NB > 7 && later >= 7) return wait_vm<7 * VM>();
-  if (NB > 6 && later >= 6) return wait_vm<6 * VM>();
-  if (NB > 5 && later >= 5) return wait_vm<5 * VM>();
-  if (NB > 4 && later >= 4) return wait_vm<4 * VM>();
-  if (NB > 3 && later >= 3) return wait_vm<3 * VM>();
-  if (later >= 2) return wait_vm<2 * VM>();
-  if (later >= 1) return wait_vm<VM>();
-  wait_vm<0>();
+  if constexpr (L == 0) {
+    wait_vm<0>();
+  } else {
+    if (later >= L) return wait_vm<L * VM>();
+    wait_landed<VM, NB, L - 1>(later);
+  }
 }
 
 __device__ __forceinline__ double xor16_sum(double v) {
@@ -124,10 +124,13 @@ __device__ __forceinline__ void dma16(const void* base, uint32_t voff, lds_doubl
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, 0, 0, 0);
 }
 
+// tall: a shard too tall for the second column's lane offset (n_pad 8 >= 2^32 - 1024) takes each
+// column of a pair in its own half-wave instruction (lanes 0..31 / 32..63, the same LDS destination:
+// the DMA writes lane-linearly), voff then holding only the row part.
 template <int P16>
 __device__ __forceinline__ void stage_r(lds_double* l3, int s, const PassArgs& a, const double* vsrc, int64_t blk,
                                         int k, int npair_stored, const uint32_t (&voff)[NR<P16>::PPW], uint32_t vvoff,
-                                        int lane) {
+                                        int lane, bool tall) {
   using G = NR<P16>;
   lds_double* dst = l3 + s * G::PER;
   const int64_t r0 = blk * SB;
@@ -135,7 +138,12 @@ __device__ __forceinline__ void stage_r(lds_double* l3, int s, const PassArgs& a
   for (int i = 0; i < G::PPW; ++i) {
     const int q = k * G::PPW + i;                                   // LDS column pair
     const int qs = __builtin_amdgcn_readfirstlane(q < npair_stored ? q : npair_stored - 1);
-    dma16(a.X + (int64_t)(2 * qs) * a.ld + r0, voff[i], dst + 2 * q * SB);
+    if (!tall) {
+      dma16(a.X + (int64_t)(2 * qs) * a.ld + r0, voff[i], dst + 2 * q * SB);
+    } else {
+      if (lane < 32) dma16(a.X + (int64_t)(2 * qs) * a.ld + r0, voff[i], dst + 2 * q * SB);
+      if (lane >= 32) dma16(a.X + (int64_t)(2 * qs + 1) * a.ld + r0, voff[i], dst + 2 * q * SB);
+    }
   }
   if (lane < 32) dma16(vsrc + r0, vvoff, dst + G::OFF_V + k * SB);
 }
@@ -213,8 +221,10 @@ __global__ void __launch_bounds__(64 * NR<P16>::NW, 3) irls_narrow_r_kernel(Pass
     // (h = lane >> 5), LDS row pair pp = lane & 31 holds source pair pp ^ ((2q + h) & 15)
     uint32_t voff[G::PPW];
     const int h = lane >> 5, pp = lane & 31;
+    const bool tall = a.ld * 8 + 1024 >= ((int64_t)1 << 32);
 #pragma unroll
-    for (int i = 0; i < G::PPW; ++i) voff[i] = (uint32_t)(h * a.ld * 8 + 16 * (pp ^ ((2 * (k * G::PPW + i) + h) & 15)));
+    for (int i = 0; i < G::PPW; ++i)
+      voff[i] = (uint32_t)((tall ? 0 : h * a.ld * 8) + 16 * (pp ^ ((2 * (k * G::PPW + i) + h) & 15)));
     uint32_t vvoff = (uint32_t)(16 * pp);
     const double* vsrc = a.y;
     if (k == 1 && a.m) vsrc = a.m;
@@ -228,9 +238,9 @@ __global__ void __launch_bounds__(64 * NR<P16>::NW, 3) irls_narrow_r_kernel(Pass
         uint32_t vt[G::PPW];
 #pragma unroll
         for (int i = 0; i < G::PPW; ++i) vt[i] = voff[i] - (pp >= 16 ? 256u : 0u);
-        stage_r<P16>(l3, s, a, vsrc, blk, k, npair_stored, vt, vvoff - (pp >= 16 ? 256u : 0u), lane);
+        stage_r<P16>(l3, s, a, vsrc, blk, k, npair_stored, vt, vvoff - (pp >= 16 ? 256u : 0u), lane, tall);
       } else {
-        stage_r<P16>(l3, s, a, vsrc, blk, k, npair_stored, voff, vvoff, lane);
+        stage_r<P16>(l3, s, a, vsrc, blk, k, npair_stored, voff, vvoff, lane, tall);
       }
     };
     const int64_t nblk = b1 - b0;
@@ -292,7 +302,9 @@ __global__ void __launch_bounds__(64 * NR<P16>::NW, 3) irls_narrow_r_kernel(Pass
     // block i = blk - b0 sits in slot i mod NB; its row stage runs on row wave i mod 4, one block
     // ahead of the Gram.  Before iteration i's restage, blocks 0 .. i + NB - 1 have been issued.
     if (nblk > 0) {
-      wait_landed<G::VMEM, NB>((int)((NB < nblk ? NB : nblk) - 1));  // this wave's part of block 0
+      const int later = (int)((NB < nblk ? NB : nblk) - 1);  // this wave's part of block 0
+      if (tall) wait_landed<G::VMEM_TALL, NB>(later);
+      else wait_landed<G::VMEM, NB>(later);
       bump(flag);
       if (k == 0) {
         spin(flag, 4u);
@@ -307,7 +319,9 @@ __global__ void __launch_bounds__(64 * NR<P16>::NW, 3) irls_narrow_r_kernel(Pass
       if (i + 1 < nblk) {  // the row stage of block i + 1
         int s1 = cur + 1 == NB ? 0 : cur + 1;
         // blocks up to i + NB - 1 are issued here (block i + NB only after block i is consumed)
-        wait_landed<G::VMEM, NB>((int)((i + NB - 1 < nblk ? i + NB - 1 : nblk - 1) - (i + 1)));
+        const int later = (int)((i + NB - 1 < nblk ? i + NB - 1 : nblk - 1) - (i + 1));
+        if (tall) wait_landed<G::VMEM_TALL, NB>(later);
+        else wait_landed<G::VMEM, NB>(later);
         bump(flag);
         if (((i + 1) & 3) == k) {
           spin(flag, (unsigned)(4 * (i + 2)));
@@ -501,8 +515,9 @@ hipError_t launch_r_p(const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0
 }  // namespace
 
 bool narrow_r_ok(int P16, int64_t n_pad) {
-  // 32-bit DMA lane offsets: the second column of a pair is ld * 8 bytes away
-  return P16 >= 2 && P16 <= 4 && n_pad > 0 && n_pad * 8 + 1024 < ((int64_t)1 << 32);
+  // any shard: one past the 32-bit lane offsets of a column pair stages a column per half-wave
+  // instruction (stage_r's tall form)
+  return P16 >= 2 && P16 <= 4 && n_pad > 0;
 }
 
 hipError_t launch_narrow_r(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {

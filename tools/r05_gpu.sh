@@ -59,3 +59,11 @@ if [[ ,$STAGES, == *,nr,* ]]; then  # split-role narrow pass: parity against irl
   timeout -k 10 300 python -u tools/nr_check.py timing > gpurun_out/nr_timing.log 2>&1 || { echo "nr timing failed"; tail -30 gpurun_out/nr_timing.log; exit 1; }
   cat gpurun_out/nr_timing.log
 fi
+if [[ ,$STAGES, == *,ab64,* ]]; then  # narrow p = 64 / 48 / 32: the A/B library (abl/base) against the tree
+  export AB_LIBS=${AB64_LIBS:-abl/base/libsglm_hip.so@SGLM_NARROW_SPLIT=0,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=${AB_REPS:-2}
+  for spec in ${AB64_CASES:-125000000:64:2:poisson:log 150000000:48:0:binomial:logit}; do
+    IFS=: read AN AP AK AF AL <<< "$spec"
+    AN=$AN AP=$AP AK=$AK AF=$AF AL=$AL timeout -k 10 300 python tools/ab.py >> gpurun_out/ab64.log 2>&1 || { echo "ab64 failed"; tail gpurun_out/ab64.log; exit 1; }
+  done
+  cat gpurun_out/ab64.log
+fi

@@ -83,7 +83,7 @@ struct NGeo {
   // covers both blocks' rows on all 64 lanes (upper half: the stashed block), then both blocks'
   // MFMAs run from registers.  Half the family-arithmetic instructions per row.
   static constexpr bool PAIR = NRB == 32;
-  static constexpr int WAVE_LDS = OFF_W + (PAIR ? 4 : 2) * NRB;  // doubles per wave
+  static constexpr int WAVE_LDS = OFF_W + 4 * NRB;  // doubles per wave (w / w*z of a block pair)
   static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
   static_assert(NW % 4 == 0, "whole waves per SIMD");
@@ -234,65 +234,111 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
   if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
 
+  // The blocks alternate the two buffers, so the loops take them in pairs with the buffer a
+  // compile-time constant: every LDS address is a per-lane base fixed for the kernel plus an immediate
+  // offset (the compiler had formed the eta reads' swizzled addresses with one v_add3 per read and
+  // block), and the DMA keeps one 64-bit source pointer per swizzle class, advanced once per block (it
+  // had carried two 64-bit adds per column group and block).
+  // eta reads: lane (g, rl), column c = LPR u + g at (c >> 4) BSTR + (c & 15) NRB + (rl ^ swz(c)); for
+  // u = EC j + k the lane part depends on k only, j moves by BSTR (immediate)
+  constexpr int EC = 16 / LPR;
+  int eoff[EC];
+#pragma unroll
+  for (int k = 0; k < EC; ++k) {
+    const int c = LPR * k + g;
+    eoff[k] = (c & 15) * NRB + (rl ^ swz<NRB>(c));
+  }
+  // Gram operand reads: lane (rq, cl) reads row 4 s + rq of column 16 b + cl
+  int goff[NRB / 4];
+#pragma unroll
+  for (int s = 0; s < NRB / 4; ++s) goff[s] = cl * NRB + ((4 * s + rq) ^ fcl);
+  // DMA sources of the next block to stage (blocks are staged in order, b0 + 2 onwards): one 64-bit
+  // pointer per swizzle class, the column group's offset added per instruction from SGPRs
+  const double* dsrc[G::LPER];
+#pragma unroll
+  for (int o = 0; o < G::LPER; ++o) dsrc[o] = a.X + (b0 + 2) * NRB + loff[o];
+  const double* vnext = vsrc + (b0 + 2) * NRB;
+  auto stage_next = [&](auto bufc) {
+    constexpr int BUFI = decltype(bufc)::value;
+    double* dst = wl + BUFI * G::BUF;
+    // the column groups' offsets are formed here on the scalar unit (an opaque copy of the stride keeps
+    // the compiler from hoisting all of them out of the loop into SGPRs, which then spilled)
+    int64_t cs = (int64_t)G::CPI * a.ld;
+    asm volatile("" : "+s"(cs));
+    int64_t co = 0;
+#pragma unroll
+    for (int o = 0; o < G::NOCT; ++o) {
+      if (o > 0 && o < ngrp_stored) co += cs;  // uniform: groups past the stored columns repeat the last
+      __builtin_amdgcn_global_load_lds((const void*)(dsrc[o % G::LPER] + co),
+                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, 0);
+    }
+#pragma unroll
+    for (int o = 0; o < G::LPER; ++o) dsrc[o] += NRB;
+    if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, 0);
+    vnext += NRB;
+  };
+  auto eta_of = [&](const double* xs) {
+    double e4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) e4[u & 3] += xs[eoff[u % EC] + (u / EC) * G::BSTR] * bcol[u];
+    double e = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+    if constexpr (LPR == 4) e = xor16_sum(e);
+    if constexpr (LPR >= 2) e = xor32_sum(e);
+    return e;
+  };
+  auto prio = [&](int64_t blk) {
+    if (NPRIO > 0) {
+      if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
   if constexpr (G::PAIR) {
     constexpr int KS = NRB / 4;
-    double xp[KS][P16];  // the stashed block's Gram operands (lane (rq, cl): row 4s + rq, column 16b + cl)
-    double eta_p = 0.0, y_p = 0.0, m_p = 1.0, off_p = 0.0, pw_p = 1.0;
-#pragma unroll
-    for (int k = 0; k < KS; ++k)
-#pragma unroll
-      for (int b = 0; b < P16; ++b) xp[k][b] = 0.0;
-#pragma unroll 1
-    for (int64_t blk = b0; blk < b1; ++blk) {
-      const int buf = (int)((blk - b0) & 1);
-      const bool second = ((blk - b0) & 1) != 0;     // uniform
-      const bool single = !second && blk + 1 >= b1;  // the range's last block has no partner
-      if (NPRIO > 0) {
-        if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-      // block blk landed; block blk+1 may still fly, and after a pair's second block its eta store
-      if (blk + 1 >= b1) wait_vm<0>();
-      else if (has_eta && !second && blk > b0) wait_vm<G::NOCT + 2>();
+    // Row pairs (NRB = 32, p <= 32): the family arithmetic would run on 32 of the wave's 64 lanes.
+    // The first block of a pair leaves its eta, row values and Gram operands in registers and
+    // releases its buffer at once; with the second block the family arithmetic covers both blocks'
+    // rows on all 64 lanes (lanes 32..63: the first block), then both blocks' MFMAs run from
+    // registers, the first block's first.
+    auto pair_blocks = [&](int64_t blk) {
+      double xp[KS][P16];  // the first block's Gram operands (lane (rq, cl): row 4s + rq, column 16b + cl)
+      double eta_p = 0.0, y_p, m_p, off_p, pw_p;
+      prio(blk);
+      // the first block landed; the second (and the last pair's eta store) may fly
+      if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
       else wait_vm<G::NOCT + 1>();
-      const double* xs = wl + buf * G::BUF;
-      const double* vv = xs + G::XB;
-      double eta = 0.0;
-      if (irls) {
-        double e4[4] = {0.0, 0.0, 0.0, 0.0};
+      {
+        const double* xs = wl;
+        const double* vv = xs + G::XB;
+        if (irls) eta_p = eta_of(xs);
+        y_p = vv[rl];
+        m_p = a.m ? vv[NRB + rl] : 1.0;
+        off_p = a.off ? vv[2 * NRB + rl] : 0.0;
+        pw_p = a.prior ? vv[3 * NRB + rl] : 1.0;
+        if (irls) eta_p = eta_p + off_p;
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-          const int c = LPR * u + g;
-          e4[u & 3] += xs[(c >> 4) * G::BSTR + (c & 15) * NRB + (rl ^ swz<NRB>(c))] * bcol[u];
-        }
-        eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
-        eta = xor32_sum(eta);  // LPR == 2: both halves hold row rl's eta
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int b = 0; b < P16; ++b) xp[k][b] = xs[goff[k] + G::BSTR * b];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blk + 2 < b1) stage_next(std::integral_constant<int, 0>{});
       }
+      // the second block landed; block blk + 2 may fly
+      if (blk + 2 < b1) wait_vm<G::NOCT + 1>();
+      else wait_vm<0>();
+      const double* xs = wl + G::BUF;
+      const double* vv = xs + G::XB;
+      double eta = irls ? eta_of(xs) : 0.0;
       const double yv = vv[rl];
       const double mv = a.m ? vv[NRB + rl] : 1.0;
       const double ov = a.off ? vv[2 * NRB + rl] : 0.0;
       const double pv = a.prior ? vv[3 * NRB + rl] : 1.0;
       if (irls) eta = eta + ov;
-      if (!second && !single) {
-        // first block of a pair: stash, release the buffer
-        eta_p = eta;
-        y_p = yv;
-        m_p = mv;
-        off_p = ov;
-        pw_p = pv;
-#pragma unroll
-        for (int k = 0; k < KS; ++k)
-#pragma unroll
-          for (int b = 0; b < P16; ++b) xp[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
-        continue;
-      }
-      // family arithmetic: lanes [0, 32) this block's row rl, lanes [32, 64) the stashed block's
+      // family arithmetic: lanes [0, 32) this block's row rl, lanes [32, 64) the first block's
       const bool hi = lane >= NRB;
-      const int64_t row = hi ? (blk - 1) * NRB + rl : blk * NRB + rl;
+      const int64_t row = hi ? blk * NRB + rl : (blk + 1) * NRB + rl;
       double w = 0.0, wz = 0.0;
-      if (!(single && hi)) {
+      {
         const double et = hi ? eta_p : eta;
         if (irls && has_eta) a.eta_out[row] = et;
         if (row < a.n) {
@@ -303,13 +349,11 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                      !IRLS, ylogy);
             if constexpr (INIT_CONST)
-              if (mode != MODE_LM_GRAM) {
-                s_ll += init_stats_const<FAM>(y, pw);
-              }
+              if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
           }
         }
       }
-      // w / w*z at [half * NRB + rl]: the stashed block in the upper half
+      // w / w*z at [half * NRB + rl]: the first block in the upper half
       wl[G::OFF_W + lane] = w;
       wl[G::OFF_W + 2 * NRB + lane] = wz;
       // this block's Gram operands into registers, then release the buffer
@@ -317,14 +361,13 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int b = 0; b < P16; ++b) xc[k][b] = xs[cl * NRB + ((4 * k + rq) ^ fcl) + G::BSTR * b];
+        for (int b = 0; b < P16; ++b) xc[k][b] = xs[goff[k] + G::BSTR * b];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (blk + 2 < b1) nstage<P16>(wl, buf, a, blk + 2, ngrp_stored, loff, vsrc, lane);
+      if (blk + 3 < b1) stage_next(std::integral_constant<int, 1>{});
       if (do_gram) {
-        // rows in order: the stashed block (upper-half w), then this one
+        // rows in order: the first block (upper-half w), then this one
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          if (h == 0 && single) continue;
 #pragma unroll
           for (int k = 0; k < KS; ++k) {
             const int r = 4 * k + rq + (h == 0 ? NRB : 0);
@@ -340,54 +383,60 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           }
         }
       }
-    }
+    };
+    // the range's last block when it has no partner: the family arithmetic on lanes [0, 32)
+    auto single_block = [&](int64_t blk) {
+      prio(blk);
+      wait_vm<0>();
+      const double* xs = wl;
+      const double* vv = xs + G::XB;
+      double eta = irls ? eta_of(xs) : 0.0;
+      const double yv = vv[rl];
+      const double mv = a.m ? vv[NRB + rl] : 1.0;
+      const double ov = a.off ? vv[2 * NRB + rl] : 0.0;
+      const double pv = a.prior ? vv[3 * NRB + rl] : 1.0;
+      if (irls) eta = eta + ov;
+      double w = 0.0, wz = 0.0;
+      if (lane < NRB) {
+        const int64_t row = blk * NRB + rl;
+        if (irls && has_eta) a.eta_out[row] = eta;
+        if (row < a.n) {
+          if constexpr (STATS)
+            pass_row_stats<FAM>(eta, yv, ov, pv, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true, ylogy);
+          else if (!(PTAB && poisson_init_row(pconst, ptab, yv, ov, pv, w, wz, s_dev, s_aux, s_ll))) {
+            pass_row(FAM, LNK, mode, eta, yv, mv, ov, pv, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
+                     !IRLS, ylogy);
+            if constexpr (INIT_CONST)
+              if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(yv, pv);
+          }
+        }
+      }
+      wl[G::OFF_W + lane] = w;
+      wl[G::OFF_W + 2 * NRB + lane] = wz;
+      if (do_gram) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const int r = 4 * k + rq;
+          const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + 2 * NRB + r];
+          double av[P16], xk[P16];
+#pragma unroll
+          for (int b = 0; b < P16; ++b) {
+            xk[b] = xs[goff[k] + G::BSTR * b];
+            av[b] = xk[b] * wr;
+            xz[b] += xk[b] * wzr;
+          }
+          gram_kstep<P16>(acc, av, xk);
+        }
+      }
+    };
+    int64_t blk = b0;
+#pragma unroll 1
+    for (; blk + 1 < b1; blk += 2) pair_blocks(blk);
+    if (blk < b1) single_block(blk);
   } else {
-  // p > 32 (NRB = 16): the blocks alternate the two buffers, so the loop takes them in pairs with the
-  // buffer a compile-time constant -- every LDS address is then a per-lane base fixed for the kernel
-  // plus an immediate offset (the compiler had formed the eta reads' swizzled addresses with one
-  // v_add3 per read and block), and the DMA keeps one 64-bit source pointer per column group, advanced
-  // once per block (it had carried two 64-bit adds per group and block).
-  // eta reads: lane (g, rl), column c = LPR u + g at (c >> 4) BSTR + (c & 15) NRB + (rl ^ swz(c)); for
-  // u = 4 j + k the lane part depends on k only, j moves by BSTR (immediate)
-  int eoff[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = LPR * k + g;
-    eoff[k] = (c & 15) * NRB + (rl ^ swz<NRB>(c));
-  }
-  // Gram operand reads: lane (rq, cl) reads row 4 s + rq of column 16 b + cl
-  int goff[NRB / 4];
-#pragma unroll
-  for (int s = 0; s < NRB / 4; ++s) goff[s] = cl * NRB + ((4 * s + rq) ^ fcl);
-  // DMA sources of the next block to stage (blocks are staged in order, b0 + 2 onwards)
-  const double* dsrc[G::NOCT];
-#pragma unroll
-  for (int o = 0; o < G::NOCT; ++o) {
-    const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
-    dsrc[o] = a.X + (b0 + 2) * NRB + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER];
-  }
-  const double* vnext = vsrc + (b0 + 2) * NRB;
-  auto stage_next = [&](auto bufc) {
-    constexpr int BUFI = decltype(bufc)::value;
-    double* dst = wl + BUFI * G::BUF;
-#pragma unroll
-    for (int o = 0; o < G::NOCT; ++o) {
-      __builtin_amdgcn_global_load_lds((const void*)dsrc[o],
-                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, 0);
-      dsrc[o] += NRB;
-    }
-    if (lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, 0);
-    vnext += NRB;
-  };
   auto block = [&](auto bufc, int64_t blk) {
     constexpr int BUFI = decltype(bufc)::value;
-    // The two waves sharing a SIMD (wv, wv ^ 4) take turns at the higher issue priority every
-    // NPRIO blocks: the arbiter otherwise favours the older wave, the younger one falls ~35 %
-    // behind on its equal share and finishes alone with no partner to overlap.
-    if (NPRIO > 0) {
-      if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
+    prio(blk);
     // block blk landed; block blk+1 (and the previous block's eta store) may still fly
     if (blk + 1 >= b1) wait_vm<0>();
     else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
@@ -395,15 +444,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     const double* xs = wl + BUFI * G::BUF;
 
     // ---- row stage ----
-    double eta = 0.0;
-    if (irls) {
-      double e4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int u = 0; u < CPL; ++u) e4[u & 3] += xs[eoff[u & 3] + (u >> 2) * G::BSTR] * bcol[u];
-      eta = (e4[0] + e4[1]) + (e4[2] + e4[3]);
-      if constexpr (LPR == 4) eta = xor16_sum(eta);
-      if constexpr (LPR >= 2) eta = xor32_sum(eta);
-    }
+    double eta = irls ? eta_of(xs) : 0.0;
     if (lane < NRB) {
       const double* vv = xs + G::XB;
       const int64_t row = blk * NRB + rl;
@@ -450,11 +491,92 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (blk + 2 < b1) stage_next(bufc);
   };
+  // Block pairs: the family arithmetic ran on 16 of the wave's 64 lanes (ablation: ~3 ms of a 15 ms
+  // p = 64 pass).  Both blocks of a pair are formed first -- eta of the first block, its row values
+  // kept in registers, eta of the second -- then the family arithmetic covers both blocks' rows on 32
+  // lanes (lanes 16..31: the first block), then the two Grams, the first block's first (the rows in
+  // the same order as block by block).  Unlike the p <= 32 loop the first block's Gram operands are
+  // not stashed in registers (at P16 = 4 they do not fit beside the accumulators): its buffer is
+  // released after its Gram, so block blk + 2's DMA flies under the second block's Gram only.
+  auto pair_blocks = [&](int64_t blk) {
+    prio(blk);
+    // the first block landed (the second and the last pair's eta store may fly)
+    if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
+    else wait_vm<G::NOCT + 1>();
+    double eta_p = 0.0, y_p, m_p, off_p, pw_p;
+    {
+      const double* xs = wl;
+      if (irls) eta_p = eta_of(xs);
+      const double* vv = xs + G::XB;
+      y_p = vv[rl];
+      m_p = a.m ? vv[NRB + rl] : 1.0;
+      off_p = a.off ? vv[2 * NRB + rl] : 0.0;
+      pw_p = a.prior ? vv[3 * NRB + rl] : 1.0;
+      if (irls) eta_p = eta_p + off_p;
+    }
+    wait_vm<0>();  // the second block landed
+    const double* xs1 = wl + G::BUF;
+    double eta = irls ? eta_of(xs1) : 0.0;
+    if (lane < 2 * NRB) {
+      // lanes [0, 16): the second block's row rl; lanes [16, 32): the first block's row rl
+      const bool hi = lane >= NRB;
+      const double* vv = xs1 + G::XB;
+      const int64_t row = hi ? blk * NRB + rl : (blk + 1) * NRB + rl;
+      double et = eta_p, y = y_p, m = m_p, off = off_p, pw = pw_p;
+      if (!hi) {
+        y = vv[rl];
+        m = a.m ? vv[NRB + rl] : 1.0;
+        off = a.off ? vv[2 * NRB + rl] : 0.0;
+        pw = a.prior ? vv[3 * NRB + rl] : 1.0;
+        et = irls ? eta + off : eta;
+      }
+      if (irls && has_eta) a.eta_out[row] = et;  // one store for the pair (row < n_pad)
+      double w = 0.0, wz = 0.0;
+      if (row < a.n) {
+        if constexpr (STATS)
+          pass_row_stats<FAM>(et, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true, ylogy);
+        else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
+          pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
+                   !IRLS, ylogy);
+          if constexpr (INIT_CONST)
+            if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
+        }
+      }
+      wl[G::OFF_W + lane] = w;
+      wl[G::OFF_W + 2 * NRB + lane] = wz;
+    }
+    // the two Grams: the first block's rows (w at [16, 32)), then the second's
+    auto gram = [&](auto bufc, int woff) {
+      constexpr int BUFI = decltype(bufc)::value;
+      const double* xs = wl + BUFI * G::BUF;
+#pragma unroll
+      for (int s2 = 0; s2 < NRB / 4; ++s2) {
+        const int r = 4 * s2 + rq + woff;
+        const double wr = wl[G::OFF_W + r], wzr = wl[G::OFF_W + 2 * NRB + r];
+        double xv[P16], av[P16];
+#pragma unroll
+        for (int b = 0; b < P16; ++b) {
+          xv[b] = xs[goff[s2] + G::BSTR * b];
+          av[b] = xv[b] * wr;
+          xz[b] += xv[b] * wzr;
+        }
+        gram_kstep<P16>(acc, av, xv);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the buffer returned
+    };
+    if (do_gram) gram(std::integral_constant<int, 0>{}, NRB);
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (blk + 2 < b1) stage_next(std::integral_constant<int, 0>{});
+    if (do_gram) gram(std::integral_constant<int, 1>{}, 0);
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (blk + 3 < b1) stage_next(std::integral_constant<int, 1>{});
+  };
+  int64_t blk = b0;
 #pragma unroll 1
-  for (int64_t blk = b0; blk < b1; blk += 2) {
-    block(std::integral_constant<int, 0>{}, blk);
-    if (blk + 1 < b1) block(std::integral_constant<int, 1>{}, blk + 1);
-  }
+  for (; blk + 1 < b1; blk += 2) pair_blocks(blk);
+  // the range's last block has no partner (outside the loop: inside it, the single-block path beside
+  // the pair path made the compiler spill at P16 = 4)
+  if (blk < b1) block(std::integral_constant<int, 0>{}, blk);
   }  // !PAIR
 
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----

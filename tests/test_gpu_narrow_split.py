@@ -48,7 +48,7 @@ CASES = [
     ("p32 logit (P16 = 2, forced)", 0, ODD, 32, "binomial", "logit", 2),
     ("p20 poisson + offset + prior (P16 = 2, forced)", 2, 100_000, 20, "poisson", "log", 2),
     ("p64 logit, fewer blocks than workgroups", 0, 3_000, 64, "binomial", "logit", 3),
-    ("p64 logit, one block", 0, 50, 64, "binomial", "logit", 3),
+    ("p20 gaussian, one block (P16 = 2, forced)", 1, 60, 20, "gaussian", "identity", 2),
 ]
 
 

@@ -4,6 +4,20 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 STAGES=${1:-cap,test,bench}
+if [[ ,$STAGES, == *,ab64,* ]]; then  # narrow p = 64 / 48 / 32: the A/B library (abl/base) against the tree
+  export AB_LIBS=${AB64_LIBS:-abl/base/libsglm_hip.so@SGLM_NARROW_SPLIT=0,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=${AB_REPS:-2}
+  for spec in ${AB64_CASES:-125000000:64:2:poisson:log 150000000:48:0:binomial:logit}; do
+    IFS=: read AN AP AK AF AL <<< "$spec"
+    AN=$AN AP=$AP AK=$AK AF=$AF AL=$AL timeout -k 10 300 python tools/ab.py >> gpurun_out/ab64.log 2>&1 || { echo "ab64 failed"; tail gpurun_out/ab64.log; exit 1; }
+  done
+  cat gpurun_out/ab64.log
+fi
+if [[ ,$STAGES, == *,nr,* ]]; then  # split-role narrow pass: parity against irls_narrow_kernel, then pass times
+  timeout -k 10 300 python -u tools/nr_check.py parity > gpurun_out/nr_parity.log 2>&1 || { echo "nr parity failed"; tail -30 gpurun_out/nr_parity.log; exit 1; }
+  cat gpurun_out/nr_parity.log
+  timeout -k 10 300 python -u tools/nr_check.py timing > gpurun_out/nr_timing.log 2>&1 || { echo "nr timing failed"; tail -30 gpurun_out/nr_timing.log; exit 1; }
+  cat gpurun_out/nr_timing.log
+fi
 if [[ ,$STAGES, == *,cap,* ]]; then
   timeout -k 10 300 python -u tools/gram_split_capture.py > gpurun_out/cap.log 2>&1 || { echo "capture failed"; tail -20 gpurun_out/cap.log; exit 1; }
   tail -3 gpurun_out/cap.log
@@ -53,17 +67,35 @@ if [[ ,$STAGES, == *,bench,* ]]; then
   timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/bench.json')); r=d['roofline']; s=d.get('strong_scaling_1b_logit') or {}; print(d['ms_per_step'], r['kernel'], r['kernel_ms'], r['frac'], d['time_to_converge_s'], s.get('ms_per_iter'), s.get('time_to_converge_s'))"
 fi
-if [[ ,$STAGES, == *,nr,* ]]; then  # split-role narrow pass: parity against irls_narrow_kernel, then pass times
-  timeout -k 10 300 python -u tools/nr_check.py parity > gpurun_out/nr_parity.log 2>&1 || { echo "nr parity failed"; tail -30 gpurun_out/nr_parity.log; exit 1; }
-  cat gpurun_out/nr_parity.log
-  timeout -k 10 300 python -u tools/nr_check.py timing > gpurun_out/nr_timing.log 2>&1 || { echo "nr timing failed"; tail -30 gpurun_out/nr_timing.log; exit 1; }
-  cat gpurun_out/nr_timing.log
-fi
-if [[ ,$STAGES, == *,ab64,* ]]; then  # narrow p = 64 / 48 / 32: the A/B library (abl/base) against the tree
-  export AB_LIBS=${AB64_LIBS:-abl/base/libsglm_hip.so@SGLM_NARROW_SPLIT=0,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=${AB_REPS:-2}
-  for spec in ${AB64_CASES:-125000000:64:2:poisson:log 150000000:48:0:binomial:logit}; do
-    IFS=: read AN AP AK AF AL <<< "$spec"
-    AN=$AN AP=$AP AK=$AK AF=$AF AL=$AL timeout -k 10 300 python tools/ab.py >> gpurun_out/ab64.log 2>&1 || { echo "ab64 failed"; tail gpurun_out/ab64.log; exit 1; }
+if [[ ,$STAGES, == *,pmcab,* ]]; then  # PMC of one workload (PMCAB_WL name:PN:PP:PKIND:PF:PL) under each library of PMCAB_LIBS
+  export TMPDIR=/tmp
+  IFS=: read -r name PN PP PKIND PF PL <<< "${PMCAB_WL:-poisson64:50000000:64:2:poisson:log}"
+  export PN PP PKIND PF PL PK=2
+  mkdir -p gpurun_out/pmcab
+  for spec in ${PMCAB_LIBS:-sparkglm_amd/lib/libsglm_hip.so}; do
+    lib=${spec%%@*}; tag=$(basename $(dirname $lib)); extra=""; [[ $spec == *@* ]] && extra=${spec#*@}
+    for grp in "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_COEXEC_CYCLES"; do
+      g=$(echo $grp | cut -c1-4); d="gpurun_out/pmcab/${name}_${tag}_$(echo $grp | md5sum | cut -c1-6)"
+      env SGLM_LIB=$lib $extra timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python tools/pass_bench.py > "$d.log" 2>&1 || { echo "pmcab $tag failed"; tail -5 "$d.log"; exit 1; }
+    done
+    echo "== $tag"; python tools/pmc_sum.py gpurun_out/pmcab/${name}_${tag}_* --kernel irls_narrow --json > gpurun_out/pmcab/${name}_${tag}.json; python - "$name" "$tag" <<'PY'
+import json, sys
+d = json.load(open(f"gpurun_out/pmcab/{sys.argv[1]}_{sys.argv[2]}.json"))
+for k, e in d.items():
+    clk = e["GRBM_GUI_ACTIVE"] / 8 / (e["avg_ms"] * 1e-3) / 1e9 if e.get("avg_ms") else 0
+    print(k[-60:], f"ms {e['avg_ms']:.3f} clk {clk:.2f}GHz valu/mfma {e['SQ_INSTS_VALU']/max(e['SQ_INSTS_MFMA'],1):.2f} "
+          f"mfma_busy {e['SQ_VALU_MFMA_BUSY_CYCLES']/(1024*clk*1e9*e['avg_ms']*1e-3):.3f} "
+          f"wait {e['SQ_WAIT_ANY']/e['SQ_WAVE_CYCLES']:.3f} waitinst {e['SQ_WAIT_INST_ANY']/e['SQ_WAVE_CYCLES']:.3f} "
+          f"active {e['SQ_ACTIVE_INST_ANY']/e['SQ_WAVE_CYCLES']:.3f} valu_act {e['SQ_ACTIVE_INST_VALU']/e['SQ_WAVE_CYCLES']:.3f} "
+          f"lds_inst {e['SQ_INSTS_LDS']:.3g} salu {e['SQ_INSTS_SALU']:.3g} coexec {e['SQ_VALU_MFMA_COEXEC_CYCLES']:.3g}")
+PY
   done
-  cat gpurun_out/ab64.log
+fi
+if [[ ,$STAGES, == *,abbit,* ]]; then  # bitwise pass hash + pass time (tools/ab_k1r.py) over ABBIT_LIBS for each ABBIT_CASES n:p:kind:fam:link
+  export AB_LIBS=${ABBIT_LIBS} AB_REPS=${AB_REPS:-2}
+  for spec in ${ABBIT_CASES:-200000000:32:0:binomial:logit}; do
+    IFS=: read AN AP AK AF AL <<< "$spec"
+    AN=$AN AP=$AP AK=$AK AF=$AF AL=$AL timeout -k 10 300 python tools/ab_k1r.py >> gpurun_out/abbit.log 2>&1 || { echo "abbit failed"; tail gpurun_out/abbit.log; exit 1; }
+  done
+  cat gpurun_out/abbit.log
 fi

@@ -14,10 +14,10 @@ from sparkglm_amd import _lib as L
 @pytest.mark.parametrize("n,p,fs,proc,force,kind,name", [
     (1_000_000, 20, 1, False, False, "narrow", "irls_narrow_kernel<2,binomial,logit>"),
     (1_000_000_000, 32, 1, False, False, "narrow", "irls_narrow_kernel<2,binomial,logit>"),
-    (125_000_000, 64, 1, False, False, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),
-    (125_000_000, 48, 1, False, False, "narrow-split", "irls_narrow_r_kernel<3,binomial,logit>"),
-    (125_000_000, 33, 1, False, False, "narrow-split", "irls_narrow_r_kernel<3,binomial,logit>"),
-    (600_000_000, 64, 1, False, False, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),  # tall form
+    (125_000_000, 64, 1, False, False, "narrow", "irls_narrow_kernel<4,binomial,logit>"),
+    (125_000_000, 48, 1, False, False, "narrow", "irls_narrow_kernel<3,binomial,logit>"),
+    (125_000_000, 33, 1, False, False, "narrow", "irls_narrow_kernel<3,binomial,logit>"),
+    (600_000_000, 64, 1, False, False, "narrow", "irls_narrow_kernel<4,binomial,logit>"),
     (10_000_000, 65, 1, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),
     (10_000_000, 80, 1, False, False, "fused", "irls_pass_kernel<5,binomial,logit>"),
     (10_000_000, 80, 5, False, False, "fused-split", "irls_pass_r_kernel<5,binomial,logit>"),
@@ -51,6 +51,9 @@ def test_kernel_choice(n, p, fs, proc, force, kind, name):
 
 @pytest.mark.parametrize("n,p,ns,kind,name", [
     (125_000_000, 64, 0, "narrow", "irls_narrow_kernel<4,binomial,logit>"),      # SGLM_NARROW_SPLIT=0: never
+    (125_000_000, 64, 3, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),
+    (125_000_000, 33, 3, "narrow-split", "irls_narrow_r_kernel<3,binomial,logit>"),
+    (600_000_000, 64, 3, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),  # tall form
     (500_000_000, 32, 2, "narrow-split", "irls_narrow_r_kernel<2,binomial,logit>"),
     (1_000_000_000, 32, 2, "narrow-split", "irls_narrow_r_kernel<2,binomial,logit>"),  # tall form
     (1_000_000, 16, 2, "narrow", "irls_narrow_kernel<1,binomial,logit>"),         # no one-block split variant
@@ -58,13 +61,14 @@ def test_kernel_choice(n, p, fs, proc, force, kind, name):
     (536_870_000, 64, 4, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),
 ])
 def test_narrow_split_choice(n, p, ns, kind, name):
-    # the split-role narrow pass (narrow_r.hip) from P16 = SGLM_NARROW_SPLIT (default 3) at any shard
+    # the split-role narrow pass (narrow_r.hip) from P16 = SGLM_NARROW_SPLIT (default 0: off,
+    # slower than irls_narrow_kernel on MI355X) at any shard
     # height (past 2^29 rows its DMA takes one column per half-wave instruction)
     assert L.pass_kernel_for(n, p, narrow_split=ns) == (kind, name)
 
 
 def test_kernel_name_carries_the_family():
-    assert L.pass_kernel_for(125_000_000, 64, "poisson", "log")[1] == "irls_narrow_r_kernel<4,poisson,log>"
+    assert L.pass_kernel_for(125_000_000, 64, "poisson", "log")[1] == "irls_narrow_kernel<4,poisson,log>"
     assert L.pass_kernel_for(1_000_000, 200, "gamma", "inverse")[1] == "irls_pass_r_kernel<13,gamma,inverse>"
 
 

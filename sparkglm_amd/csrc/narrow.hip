@@ -277,14 +277,27 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, 0);
     vnext += NRB;
   };
+  // eta: every LDS read of the row's columns issued before the first FMA (the scheduler had
+  // interleaved them one read, one wait, one FMA -- CPL dependent LDS round trips per block)
   auto eta_of = [&](const double* xs) {
     double e4[4] = {0.0, 0.0, 0.0, 0.0};
+    double xv[CPL];
 #pragma unroll
-    for (int u = 0; u < CPL; ++u) e4[u & 3] += xs[eoff[u % EC] + (u / EC) * G::BSTR] * bcol[u];
+    for (int u = 0; u < CPL; ++u) xv[u] = xs[eoff[u % EC] + (u / EC) * G::BSTR];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) e4[u & 3] += xv[u] * bcol[u];
     double e = (e4[0] + e4[1]) + (e4[2] + e4[3]);
     if constexpr (LPR == 4) e = xor16_sum(e);
     if constexpr (LPR >= 2) e = xor32_sum(e);
     return e;
+  };
+  // a block's m / offset / prior slots always hold data (absent vectors: y again, nstage), so they are
+  // read unconditionally and selected: no scalar branch per value between the row stage's LDS reads
+  const bool hm = a.m != nullptr, ho = a.off != nullptr, hp = a.prior != nullptr;
+  auto rowv = [&](const double* vv, int k, bool present, double dflt) {
+    const double v = vv[k * NRB + rl];
+    return present ? v : dflt;
   };
   auto prio = [&](int64_t blk) {
     if (NPRIO > 0) {
@@ -312,9 +325,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         const double* vv = xs + G::XB;
         if (irls) eta_p = eta_of(xs);
         y_p = vv[rl];
-        m_p = a.m ? vv[NRB + rl] : 1.0;
-        off_p = a.off ? vv[2 * NRB + rl] : 0.0;
-        pw_p = a.prior ? vv[3 * NRB + rl] : 1.0;
+        m_p = rowv(vv, 1, hm, 1.0);
+        off_p = rowv(vv, 2, ho, 0.0);
+        pw_p = rowv(vv, 3, hp, 1.0);
         if (irls) eta_p = eta_p + off_p;
 #pragma unroll
         for (int k = 0; k < KS; ++k)
@@ -330,9 +343,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       const double* vv = xs + G::XB;
       double eta = irls ? eta_of(xs) : 0.0;
       const double yv = vv[rl];
-      const double mv = a.m ? vv[NRB + rl] : 1.0;
-      const double ov = a.off ? vv[2 * NRB + rl] : 0.0;
-      const double pv = a.prior ? vv[3 * NRB + rl] : 1.0;
+      const double mv = rowv(vv, 1, hm, 1.0);
+      const double ov = rowv(vv, 2, ho, 0.0);
+      const double pv = rowv(vv, 3, hp, 1.0);
       if (irls) eta = eta + ov;
       // family arithmetic: lanes [0, 32) this block's row rl, lanes [32, 64) the first block's
       const bool hi = lane >= NRB;
@@ -392,9 +405,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       const double* vv = xs + G::XB;
       double eta = irls ? eta_of(xs) : 0.0;
       const double yv = vv[rl];
-      const double mv = a.m ? vv[NRB + rl] : 1.0;
-      const double ov = a.off ? vv[2 * NRB + rl] : 0.0;
-      const double pv = a.prior ? vv[3 * NRB + rl] : 1.0;
+      const double mv = rowv(vv, 1, hm, 1.0);
+      const double ov = rowv(vv, 2, ho, 0.0);
+      const double pv = rowv(vv, 3, hp, 1.0);
       if (irls) eta = eta + ov;
       double w = 0.0, wz = 0.0;
       if (lane < NRB) {
@@ -450,14 +463,14 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       const int64_t row = blk * NRB + rl;
       double w = 0.0, wz = 0.0;
       if (irls) {
-        eta = eta + (a.off ? vv[2 * NRB + rl] : 0.0);
+        eta = eta + rowv(vv, 2, ho, 0.0);
         if (has_eta) a.eta_out[row] = eta;  // always issued (row < n_pad): keeps vmcnt exact
       }
       if (row < a.n) {
         const double y = vv[rl];
-        const double m = a.m ? vv[NRB + rl] : 1.0;
-        const double off = a.off ? vv[2 * NRB + rl] : 0.0;
-        const double pw = a.prior ? vv[3 * NRB + rl] : 1.0;
+        const double m = rowv(vv, 1, hm, 1.0);
+        const double off = rowv(vv, 2, ho, 0.0);
+        const double pw = rowv(vv, 3, hp, 1.0);
         if constexpr (STATS)
           pass_row_stats<FAM>(eta, y, off, pw, w, wz, s_dev, s_aux, s_pear, s_ll, s_bad, true, ylogy);
         else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
@@ -500,18 +513,21 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   // released after its Gram, so block blk + 2's DMA flies under the second block's Gram only.
   auto pair_blocks = [&](int64_t blk) {
     prio(blk);
-    // the first block landed (the second and the last pair's eta store may fly)
-    if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
-    else wait_vm<G::NOCT + 1>();
+    // the first block landed, the second may fly.  The last pair's eta store was issued before both
+    // blocks' DMAs (in its row stage, ahead of the Grams), so it is older than the first block's and
+    // must not be counted as in flight: with NOCT + 2 the first block's row-vector DMA (y, offset,
+    // prior) could still be landing while the row stage read it (a run-to-run difference of ~1e-6
+    // in the Poisson / Gaussian passes at p > 32, tests/test_gpu_determinism.py)
+    wait_vm<G::NOCT + 1>();
     double eta_p = 0.0, y_p, m_p, off_p, pw_p;
     {
       const double* xs = wl;
       if (irls) eta_p = eta_of(xs);
       const double* vv = xs + G::XB;
       y_p = vv[rl];
-      m_p = a.m ? vv[NRB + rl] : 1.0;
-      off_p = a.off ? vv[2 * NRB + rl] : 0.0;
-      pw_p = a.prior ? vv[3 * NRB + rl] : 1.0;
+      m_p = rowv(vv, 1, hm, 1.0);
+      off_p = rowv(vv, 2, ho, 0.0);
+      pw_p = rowv(vv, 3, hp, 1.0);
       if (irls) eta_p = eta_p + off_p;
     }
     wait_vm<0>();  // the second block landed
@@ -525,9 +541,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       double et = eta_p, y = y_p, m = m_p, off = off_p, pw = pw_p;
       if (!hi) {
         y = vv[rl];
-        m = a.m ? vv[NRB + rl] : 1.0;
-        off = a.off ? vv[2 * NRB + rl] : 0.0;
-        pw = a.prior ? vv[3 * NRB + rl] : 1.0;
+        m = rowv(vv, 1, hm, 1.0);
+        off = rowv(vv, 2, ho, 0.0);
+        pw = rowv(vv, 3, hp, 1.0);
         et = irls ? eta + off : eta;
       }
       if (irls && has_eta) a.eta_out[row] = et;  // one store for the pair (row < n_pad)

@@ -128,16 +128,23 @@ def _fail_worker(rank, world, port, case, q):
         dist.destroy_process_group()
         return
     eng.set_comm(D.torch_allreduce(), on_device=True, rank=rank)
+
+    def put_and_exit(item):
+        # os._exit skips the queue's feeder thread: flush the item to the pipe first
+        q.put(item)
+        q.close()
+        q.join_thread()
+        os._exit(0)
+
     if rank == 1:
-        q.put((rank, "exited"))
-        os._exit(0)  # dies before the fit's first collective
+        put_and_exit((rank, "exited"))  # dies before the fit's first collective
     t0 = time.perf_counter()
     try:
         eng.fit_glm("poisson", "log", init="multiple")
-        q.put((rank, "no error"))
+        item = (rank, "no error")
     except CommError as exc:
-        q.put((rank, f"ecomm:{time.perf_counter() - t0:.1f}:{exc}"))
-    os._exit(0)  # the gloo group lost a member: skip its teardown
+        item = (rank, f"ecomm:{time.perf_counter() - t0:.1f}:{exc}")
+    put_and_exit(item)  # the gloo group lost a member: skip its teardown
 
 
 @pytest.mark.parametrize("case", ["badrank", "deadpeer"])

@@ -42,11 +42,14 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Issue priority of the two waves of a SIMD alternates every NPRIO blocks (2 / 8 / 16 measured
-// equal or slower).  Measured and not kept (DESIGN.md 4 K1'): the diagonal tiles on three
+// Issue priority by phase: a wave runs its row stage (eta, the family arithmetic: a dependent fp64
+// chain) at high priority and its Grams at low, so the partner wave's MFMA stream fills the row
+// stage's latencies instead of delaying its instructions (round 5: p = 32 -2 %, p = 48 -1 %, p = 64
+// +-0 against priorities alternating between the two waves every 4 blocks; 12 waves a CU on 8-row
+// blocks at p > 32: +18-20 %, DESIGN.md 4 K1').  Measured and not kept: the diagonal tiles on three
 // v_mfma_f64_4x4x4f64 (rotated B operands from LDS or by DPP: slower at p = 32 and 64); a
 // batched Gram phase (all operands, then all VALU, then all MFMAs per block: p = 64 +25 %).
-constexpr int NPRIO = 4;
+constexpr int PRIO_ROWS = 2, PRIO_GRAM = 0;
 
 // Rows per block NRB: 32 for p <= 32 (the family arithmetic then runs on 32 lanes), 16 above
 // (LDS: 8 waves x 2 buffers).  Row swizzle f(c): 2((c >> 1) & 7) at NRB = 16 (the column
@@ -299,12 +302,6 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     const double v = vv[k * NRB + rl];
     return present ? v : dflt;
   };
-  auto prio = [&](int64_t blk) {
-    if (NPRIO > 0) {
-      if ((((blk - b0) / NPRIO) ^ (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-  };
 
   if constexpr (G::PAIR) {
     constexpr int KS = NRB / 4;
@@ -316,7 +313,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     auto pair_blocks = [&](int64_t blk) {
       double xp[KS][P16];  // the first block's Gram operands (lane (rq, cl): row 4s + rq, column 16b + cl)
       double eta_p = 0.0, y_p, m_p, off_p, pw_p;
-      prio(blk);
+      __builtin_amdgcn_s_setprio(PRIO_ROWS);
       // the first block landed; the second (and the last pair's eta store) may fly
       if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
       else wait_vm<G::NOCT + 1>();
@@ -377,6 +374,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         for (int b = 0; b < P16; ++b) xc[k][b] = xs[goff[k] + G::BSTR * b];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (blk + 3 < b1) stage_next(std::integral_constant<int, 1>{});
+      __builtin_amdgcn_s_setprio(PRIO_GRAM);
       if (do_gram) {
         // rows in order: the first block (upper-half w), then this one
 #pragma unroll
@@ -399,7 +397,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     };
     // the range's last block when it has no partner: the family arithmetic on lanes [0, 32)
     auto single_block = [&](int64_t blk) {
-      prio(blk);
+      __builtin_amdgcn_s_setprio(PRIO_ROWS);
       wait_vm<0>();
       const double* xs = wl;
       const double* vv = xs + G::XB;
@@ -426,6 +424,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       }
       wl[G::OFF_W + lane] = w;
       wl[G::OFF_W + 2 * NRB + lane] = wz;
+      __builtin_amdgcn_s_setprio(PRIO_GRAM);
       if (do_gram) {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
@@ -449,7 +448,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   } else {
   auto block = [&](auto bufc, int64_t blk) {
     constexpr int BUFI = decltype(bufc)::value;
-    prio(blk);
+    __builtin_amdgcn_s_setprio(PRIO_ROWS);
     // block blk landed; block blk+1 (and the previous block's eta store) may still fly
     if (blk + 1 >= b1) wait_vm<0>();
     else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
@@ -485,6 +484,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     }
 
     // ---- Gramian: NRB/4 k-steps of 4 rows ----
+    __builtin_amdgcn_s_setprio(PRIO_GRAM);
     if (do_gram) {
 #pragma unroll
       for (int s = 0; s < NRB / 4; ++s) {
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   // not stashed in registers (at P16 = 4 they do not fit beside the accumulators): its buffer is
   // released after its Gram, so block blk + 2's DMA flies under the second block's Gram only.
   auto pair_blocks = [&](int64_t blk) {
-    prio(blk);
+    __builtin_amdgcn_s_setprio(PRIO_ROWS);
     // the first block landed, the second may fly.  The last pair's eta store was issued before both
     // blocks' DMAs (in its row stage, ahead of the Grams), so it is older than the first block's and
     // must not be counted as in flight: with NOCT + 2 the first block's row-vector DMA (y, offset,
@@ -580,6 +580,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the buffer returned
     };
+    __builtin_amdgcn_s_setprio(PRIO_GRAM);
     if (do_gram) gram(std::integral_constant<int, 0>{}, NRB);
     else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (blk + 2 < b1) stage_next(std::integral_constant<int, 0>{});

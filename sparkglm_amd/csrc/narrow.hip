@@ -136,14 +136,37 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
     __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
 }
 
+// Lane l of a 16-lane row takes the value of lane l & ~12 (the first 4-lane group's lane of the same
+// position): ds_swizzle in bit mode, and_mask 0b10011 on the lane id within 32.
+__device__ __forceinline__ double bcast_quad0(double v) {
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x13);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x13);
+  return __hiloint2double(hi, lo);
+}
+
 // One k-step (4 rows) of the lower-triangular Gram on v_mfma_f64_16x16x4_f64.
-template <int P16>
+// T4 (P16 = 2, p <= 20: the second column block holds at most 4 real columns, 16..19): the two
+// tiles of that block's row run on v_mfma_f64_4x4x4f64, which takes its operands in the 16x16x4
+// lane layout with 4x4 block j on columns 4j..4j+3 (tools/mfma_layout.hip) and writes block j's
+// D(m, n) to lane 16 m + 4 j + n -- exactly where the 16x16x4 tile keeps rows 0..3 of its D in
+// acc[t][0].  Tile (1, 1): block 0 is columns 16..19 x 16..19; tile (1, 0): the A operand's first
+// 4-lane group (columns 16..19) broadcast to all four groups gives columns 16..19 x 4j..4j+3 in
+// block j.  16 MFMA cycles each instead of 64 (the LM Gram of configs[0], p = 20: 96 per k-step
+// instead of 192); rows 4..15 of those tiles (columns 20..31: padding) are never formed.
+template <int P16, bool T4 = false>
 __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double (&av)[P16], const double (&xv)[P16]) {
-  int t = 0;
+  if constexpr (T4) {
+    static_assert(P16 == 2, "T4: two column blocks");
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], xv[0], acc[0], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(bcast_quad0(av[1]), xv[0], acc[1][0], 0, 0, 0);
+    acc[2][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[1], xv[1], acc[2][0], 0, 0, 0);
+  } else {
+    int t = 0;
 #pragma unroll
-  for (int bi = 0; bi < P16; ++bi)
+    for (int bi = 0; bi < P16; ++bi)
 #pragma unroll
-    for (int bj = 0; bj <= bi; ++bj, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+      for (int bj = 0; bj <= bi; ++bj, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], xv[bj], acc[t], 0, 0, 0);
+  }
 }
 
 // IRLS: compile-time a.mode == MODE_IRLS (the iterations); the init and LM Gram passes run the
@@ -154,7 +177,7 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 // carries them (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass, ~1 % at p = 64).
 // The Poisson / Gamma statistics' per-fit constants (rowmath.hpp init_stats_const) are summed by
 // the initial pass (IRLS = false) into S_AUX2.
-template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false>
+template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false, bool T4 = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
@@ -390,7 +413,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
               av[b] = xk[b] * wr;
               xz[b] += xk[b] * wzr;
             }
-            gram_kstep<P16>(acc, av, xk);
+            gram_kstep<P16, T4>(acc, av, xk);
           }
         }
       }
@@ -437,7 +460,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
             av[b] = xk[b] * wr;
             xz[b] += xk[b] * wzr;
           }
-          gram_kstep<P16>(acc, av, xk);
+          gram_kstep<P16, T4>(acc, av, xk);
         }
       }
     };
@@ -497,7 +520,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
-        gram_kstep<P16>(acc, av, xv);
+        gram_kstep<P16, T4>(acc, av, xv);
       }
     }
     // every LDS read of this buffer has returned before the DMA may overwrite it
@@ -576,7 +599,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
         }
-        gram_kstep<P16>(acc, av, xv);
+        gram_kstep<P16, T4>(acc, av, xv);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the buffer returned
     };
@@ -687,6 +710,15 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 template <int P16, int FAM, int LNK>
 void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   constexpr bool SP = stats_in_pass_family(FAM, LNK);
+  if constexpr (P16 == 2 && FAM == FAM_GAUSSIAN) {  // LM Gram / gaussian at p <= 20 (gram_kstep T4)
+    if (a.p <= 20) {
+      if (a.mode == MODE_IRLS)
+        hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, false, true>), gr, bl, 0, st, e0, e1, 0, a);
+      else
+        hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false, false, true>), gr, bl, 0, st, e0, e1, 0, a);
+      return;
+    }
+  }
   if (a.mode == MODE_IRLS && SP && a.stats_in_pass && !(FAM == FAM_BINOMIAL && a.m))
     hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, true, SP>), gr, bl, 0, st, e0, e1, 0, a);
   else if (a.mode == MODE_IRLS)

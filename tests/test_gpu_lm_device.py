@@ -118,3 +118,24 @@ def test_rank_deficient_design_takes_the_host_path(kind):
         assert not isinstance(fh, type)
         _same(fd, fh)
         assert out[True][1]["lm_device_reruns"] == 1  # the host's coefficients, the host's residual pass
+
+
+@pytest.mark.parametrize("p", [17, 18, 19, 20, 21])
+def test_last_column_block_on_4x4_mfma_matches_the_oracle(p):
+    """p <= 20 runs the LM Gram (and the gaussian passes) with the second column block's two tiles on
+    v_mfma_f64_4x4x4f64 (narrow.hip gram_kstep T4); p = 21 is the first width back on 16x16x4."""
+    rng = np.random.default_rng(100 + p)
+    n = 200_003
+    X = np.column_stack([np.ones(n), rng.uniform(-1, 1, (n, p - 1))])
+    y = X @ rng.normal(size=p) + rng.uniform(-1, 1, n)
+    with Engine(0) as e:
+        e.set_data(X, y)
+        f = e.fit_lm()
+        g = e.fit_glm("gaussian", "identity")
+    r = po.fit_lm(X, y, nthreads=8)
+    assert rel(f.coefs, r["coefs"]) < 1e-9 and rel(f.stderr, r["stderr"]) < 1e-9
+    assert rel([f.sse, f.r2, f.fstat, f.sigma], [r["sse"], r["r2"], r["fstat"], r["sigma"]]) < 1e-9
+    o = po.fit_glm(X, y, "gaussian", "identity", nthreads=8)
+    assert g.iter == o.iter
+    assert rel(g.coefs, o.coefs) < 1e-9 and rel(g.stderr, o.stderr) < 1e-9
+    assert rel([g.deviance, g.null_deviance], [o.deviance, o.null_deviance]) < 1e-9

@@ -408,13 +408,17 @@ struct sglm_engine : public Backend {
   int64_t ch_rows = 0;  // rows per chunk (multiple of 32); 0: in-kernel generation (PROC kernels)
   int nch = 0;
   std::vector<hipEvent_t> evch;  // [4 * nch + 1]: row span, Gram span per chunk; st -> st2 fork
+  std::vector<hipEvent_t> evdg;  // [nch]: chunk c's diagonal launch done (SGLM_PROC_OV_GATE)
   double *dxsc = nullptr, *dchunks = nullptr;
   bool allow_chunks = true;  // SGLM_PROC_CHUNKS=0 disables
-  // SGLM_PROC_OVERLAP: chunks of an overlapped procedural pass (<= 1: one buffer, serial).  Off:
-  // measured (250M x 512 logit) 1257 ms per pass serial, 1420 / 1480 ms at 8 / 16 chunks -- the
-  // generating row kernel's integer + fp64 VALU shares the SIMDs with the Gram's MFMAs and slows
-  // them by 31-38 %, more than the 193 ms of row kernels it hides.
-  int proc_ov_want = 0;
+  // SGLM_PROC_OVERLAP: chunks of an overlapped procedural pass (<= 1: one buffer, serial).  Round 2
+  // measured it slower beside both Gram launches (250M x 512 logit: 1257 ms per pass serial, 1420 /
+  // 1480 at 8 / 16 chunks -- the generator's integer + fp64 VALU slowed the Gram by 31-38 %).  Round 5
+  // (VERDICT r4 item 6): gated to the off-diagonal launches (SGLM_PROC_OV_GATE; the diagonal launch
+  // goes first) and the generating row kernel at raised priority, 8 chunks: 1284.5 -> 1266.9 ms on one
+  // box (ungated 1466.3, gated at normal priority 1285.7).
+  int proc_ov_want = 8;
+  bool proc_ov_gate = true;  // SGLM_PROC_OV_GATE: overlapped row kernels beside the off-diagonal launches only
   bool proc_ov = false;      // double-buffered scratch, row kernels on st2 (as the resident overlap below)
   int64_t proc_ov_min = (int64_t)1 << 20;  // SGLM_PROC_OV_MIN: fewest rows per overlapped chunk
   // resident wide shards, overlapped passes: the rows are cut into nov chunks; the row kernel of
@@ -529,6 +533,8 @@ struct sglm_engine : public Backend {
     comm.nccl = nullptr;
     for (hipEvent_t e : evch) (void)hipEventDestroy(e);
     evch.clear();
+    for (hipEvent_t e : evdg) (void)hipEventDestroy(e);
+    evdg.clear();
     for (hipEvent_t e : evov) (void)hipEventDestroy(e);
     evov.clear();
     if (st2) (void)hipStreamDestroy(st2);
@@ -883,6 +889,11 @@ struct sglm_engine : public Backend {
       hipEvent_t e = nullptr;
       HIPCHK(hipEventCreate(&e));
       evch.push_back(e);
+    }
+    while (evdg.size() < (size_t)nch) {
+      hipEvent_t e = nullptr;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      evdg.push_back(e);
     }
     HIPCHK(hipStreamSynchronize(st));
     return ensure_wide_workspace();  // the Gram schedule for ch_rows-row chunks
@@ -1358,6 +1369,9 @@ struct sglm_engine : public Backend {
           r.row_partials = proc_ov ? rowpart(c) : drp;
           // buffer c & 1 is free once the Gram kernels of chunk c - 2 are done with it
           if (proc_ov && c >= 2) HIPCHK(hipStreamWaitEvent(st2, evch[(size_t)4 * (c - 2) + 3], 0));
+          // gated: the row kernel of chunk c starts once chunk c - 1's diagonal launch is done, so it
+          // runs beside that chunk's off-diagonal launch only (the diagonal launch goes first)
+          if (proc_ov && proc_ov_gate && c >= 1) HIPCHK(hipStreamWaitEvent(st2, evdg[(size_t)c - 1], 0));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c], rs));
           HIPCHK(launch_wide_rows(r, proc_ov && c > 0 ? rgrid_ov : rgrid, rs, proc_ov && c > 0));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 1], rs));
@@ -1366,12 +1380,17 @@ struct sglm_engine : public Backend {
           g.X = xs;
           g.w = dw + r.r_begin;
           g.wz = dwz + r.r_begin;
-          for (int kind = 0; kind < 2 && !dev_only; ++kind) {
-            if (!has_sched[kind]) continue;
-            g.pieces = dpieces[kind];
-            g.wg_begin = dwgb[kind];
-            HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+          const bool gate = proc_ov && proc_ov_gate;
+          for (int q = 0; q < 2 && !dev_only; ++q) {
+            const int kind = gate ? 1 - q : q;  // gated: diagonal first
+            if (has_sched[kind]) {
+              g.pieces = dpieces[kind];
+              g.wg_begin = dwgb[kind];
+              HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
+            }
+            if (gate && kind == 1) HIPCHK(hipEventRecord(evdg[(size_t)c], st));
           }
+          if (gate && dev_only) HIPCHK(hipEventRecord(evdg[(size_t)c], st));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 3], st));
           HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, r.row_partials, proc_ov && c > 0 ? rgrid_ov : rgrid,
                                     dchunks + (int64_t)c * plen, st));
@@ -1985,6 +2004,7 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
+  if (const char* pg = std::getenv("SGLM_PROC_OV_GATE")) h->proc_ov_gate = std::atoi(pg) != 0;
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));

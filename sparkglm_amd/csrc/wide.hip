@@ -487,8 +487,13 @@ __global__ void __launch_bounds__(256) wide_rows_kernel(WideRowArgs a) {
 // beside the two persistent Gram workgroups, so at most 96 VGPRs (2 x 208 + 96 = the SIMD's
 // 512) and two rows per thread (no spills at that budget).  Per-row arithmetic and order are the
 // full kernel's, bit for bit.  Non-temporal X loads keep the Gram's rows in the caches.
+// Procedural chunks (xs_out: the design generated into the scratch beside the previous chunk's
+// off-diagonal Gram launch) run at raised issue priority: the generator's integer chain is the
+// longer of the two there (round 5, 250M x 512: 1284.5 -> 1266.9 ms per pass against no overlap;
+// at normal priority 1285.7, the row kernels spanning 862 ms beside 1124 ms of Gram).
 template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) wide_rows_ov_kernel(WideRowArgs a) {
+  if (a.xs_out) __builtin_amdgcn_s_setprio(1);
   wide_rows_body<FAM, LNK, 2, true>(a);
 }
 

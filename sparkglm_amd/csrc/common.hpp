@@ -29,6 +29,12 @@ constexpr bool stats_in_pass_family(int fam, int lnk) {
          (fam == FAM_GAMMA && lnk == LNK_INVERSE);
 }
 
+// Cache policy of the design-streaming LDS-DMA (global_load_lds aux): non-temporal.  Every byte of X
+// is read once per pass, so it should not displace what the caches hold (round 5, same box: 1B x 32
+// logit pass 45.92 -> 44.84 ms, 200M x 32 -1.0 %, 125M x 64 Poisson -0.4 %, 30M x 256 -0.6 %,
+// bitwise the default policy).  The wide path's panels are re-read by several super-tiles: default there.
+constexpr int DMA_NT = 2;
+
 // Largest column-block count of the fused (single-panel) kernel: p <= 16*16 = 256.
 constexpr int MAX_P16 = 16;
 

@@ -237,8 +237,7 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
     const int qs = __builtin_amdgcn_readfirstlane(q < a.nq ? q : a.nq - 1);  // quads past p: duplicates
     const int srow = (2 * i) ^ ((8 * q + 2 * cq) & 31);        // slot swizzle of column 4q + cq
     const double* src = lbase + (int64_t)(4 * qs) * a.ld + srow;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128), 16, 0,
-                                     0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128), 16, 0, DMA_NT);
   }
 #pragma unroll
   for (int k = 0; k < G::VMAX; ++k) {
@@ -251,7 +250,7 @@ __device__ __forceinline__ void stage_block(double* lds, int buf, const PassArgs
     if (v == 3 && a.prior) src = a.prior;
     if (lane < 16) {
       __builtin_amdgcn_global_load_lds((const void*)(src + r0 + 2 * lane),
-                                       (lds_void*)(l3 + G::OFF_V + buf * 4 * RB + v * RB), 16, 0, 0);
+                                       (lds_void*)(l3 + G::OFF_V + buf * 4 * RB + v * RB), 16, 0, DMA_NT);
     }
   }
 }
@@ -723,8 +722,7 @@ __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassAr
     const int q = q0 + k;
     const int qs = q < a.nq ? q : a.nq - 1;  // quads past p: duplicates
     const char* sb = (const char*)(a.X + (int64_t)(4 * qs) * a.ld + r0);
-    __builtin_amdgcn_global_load_lds((const void*)(sb + voff[q & 3]), (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128),
-                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(sb + voff[q & 3]), (lds_void*)(xdst + (q >> 2) * G::BSTR + (q & 3) * 128), 16, 0, DMA_NT);
   }
   const double* src = a.y;
   if (si == 1 && a.m) src = a.m;
@@ -732,8 +730,7 @@ __device__ __forceinline__ void stage_block_r(double* lds, int buf, const PassAr
   if (si == 3 && a.prior) src = a.prior;
   const char* sb = (const char*)(src + r0);
   if ((int)vvoff < 16 * 16)
-    __builtin_amdgcn_global_load_lds((const void*)(sb + vvoff), (lds_void*)(l3 + GeoR<P16>::OFF_V + buf * 4 * RB + si * RB), 16,
-                                     0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vvoff), (lds_void*)(l3 + GeoR<P16>::OFF_V + buf * 4 * RB + si * RB), 16, 0, DMA_NT);
 }
 
 // Row stage of K1r: K1's row_stage (the same lanes, partial sums and reduction order, so w, w*z

@@ -129,11 +129,10 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
   for (int o = 0; o < G::NOCT; ++o) {
     const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
     __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER]),
-                                     (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16,
-                                     0, 0);
+                                     (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16, 0, DMA_NT);
   }
   if (G::NRB == 32 || lane < 2 * G::NRB)
-    __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, DMA_NT);
 }
 
 // Lane l of a 16-lane row takes the value of lane l & ~12 (the first 4-lane group's lane of the same
@@ -296,11 +295,11 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     for (int o = 0; o < G::NOCT; ++o) {
       if (o > 0 && o < ngrp_stored) co += cs;  // uniform: groups past the stored columns repeat the last
       __builtin_amdgcn_global_load_lds((const void*)(dsrc[o % G::LPER] + co),
-                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, 0);
+                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, DMA_NT);
     }
 #pragma unroll
     for (int o = 0; o < G::LPER; ++o) dsrc[o] += NRB;
-    if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, 0);
+    if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, DMA_NT);
     vnext += NRB;
   };
   // eta: every LDS read of the row's columns issued before the first FMA (the scheduler had

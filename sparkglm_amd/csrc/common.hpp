@@ -99,6 +99,18 @@ struct WideRowArgs {
   int64_t r_begin, r_end;  // rows [r_begin, r_end) of this launch (multiples of 4; r_end may pass n_pad)
   double* xs_out;       // procedural chunks: the generated X rows stored here (column-major,
   int64_t xs_ld;        //   leading dimension xs_ld, local row = row - r_begin), else null
+  const double* eta_in; // procedural chunks after proc_gen_kernel: X beta of rows < n (MODE_IRLS), else null
+};
+
+// Procedural chunks: the lean generator (wide.hip proc_gen_kernel) -- X rows [r_begin, r_end) into
+// the scratch and X beta (no offset) of the rows < proc.n into eta_raw.
+struct ProcGenArgs {
+  ProcX proc;
+  const double* beta;   // device [p], or null (no eta: the initial pass)
+  double* xs;           // scratch, column-major, leading dimension xs_ld, local row = row - r_begin
+  int64_t xs_ld;
+  int64_t r_begin, r_end;
+  double* eta_raw;      // [n], global row index
 };
 
 // One run of 16-row blocks of one super-tile, processed by one workgroup of the persistent

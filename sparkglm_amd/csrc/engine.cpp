@@ -418,7 +418,10 @@ struct sglm_engine : public Backend {
   // goes first) and the generating row kernel at raised priority, 8 chunks: 1284.5 -> 1266.9 ms on one
   // box (ungated 1466.3, gated at normal priority 1285.7).
   int proc_ov_want = 8;
-  bool proc_ov_gate = true;  // SGLM_PROC_OV_GATE: overlapped row kernels beside the off-diagonal launches only
+  // SGLM_PROC_OV_GATE: the diagonal launch of every chunk first (1, 2; 0: off-diagonal first), and
+  // (1) the row kernel of chunk c + 1 held until chunk c's diagonal launch is done
+  int proc_ov_gate = 2;
+  int proc_lean = 1;  // SGLM_PROC_LEAN: chunks >= 1 generate in proc_gen_kernel (1), chunk 0 too (2), off (0)
   bool proc_ov = false;      // double-buffered scratch, row kernels on st2 (as the resident overlap below)
   int64_t proc_ov_min = (int64_t)1 << 20;  // SGLM_PROC_OV_MIN: fewest rows per overlapped chunk
   // resident wide shards, overlapped passes: the rows are cut into nov chunks; the row kernel of
@@ -1371,9 +1374,27 @@ struct sglm_engine : public Backend {
           if (proc_ov && c >= 2) HIPCHK(hipStreamWaitEvent(st2, evch[(size_t)4 * (c - 2) + 3], 0));
           // gated: the row kernel of chunk c starts once chunk c - 1's diagonal launch is done, so it
           // runs beside that chunk's off-diagonal launch only (the diagonal launch goes first)
-          if (proc_ov && proc_ov_gate && c >= 1) HIPCHK(hipStreamWaitEvent(st2, evdg[(size_t)c - 1], 0));
+          if (proc_ov && proc_ov_gate == 1 && c >= 1) HIPCHK(hipStreamWaitEvent(st2, evdg[(size_t)c - 1], 0));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c], rs));
-          HIPCHK(launch_wide_rows(r, proc_ov && c > 0 ? rgrid_ov : rgrid, rs, proc_ov && c > 0));
+          if (!dev_only && proc_ov && proc_lean > (c > 0 ? 0 : 1)) {
+            // the lean generator (X into the scratch, X beta into deta), then the family stage from deta
+            ProcGenArgs pg{};
+            pg.proc = procx;
+            pg.beta = mode == MODE_IRLS ? r.beta : nullptr;
+            pg.xs = xs;
+            pg.xs_ld = ch_rows;
+            pg.r_begin = r.r_begin;
+            pg.r_end = r.r_end;
+            pg.eta_raw = deta;
+            HIPCHK(launch_proc_gen(pg, c > 0 ? 2 * ncu : rgrid, rs));
+            WideRowArgs rf = r;
+            rf.xs_out = nullptr;
+            rf.proc = ProcX{};
+            rf.eta_in = mode == MODE_IRLS ? deta : nullptr;
+            HIPCHK(launch_wide_rows(rf, c > 0 ? rgrid_ov : rgrid, rs, c > 0));
+          } else {
+            HIPCHK(launch_wide_rows(r, proc_ov && c > 0 ? rgrid_ov : rgrid, rs, proc_ov && c > 0));
+          }
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 1], rs));
           if (proc_ov) HIPCHK(hipStreamWaitEvent(st, evch[(size_t)4 * c + 1], 0));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 2], st));
@@ -2004,7 +2025,8 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
-  if (const char* pg = std::getenv("SGLM_PROC_OV_GATE")) h->proc_ov_gate = std::atoi(pg) != 0;
+  if (const char* pg = std::getenv("SGLM_PROC_OV_GATE")) h->proc_ov_gate = std::atoi(pg);
+  if (const char* pl = std::getenv("SGLM_PROC_LEAN")) h->proc_lean = std::atoi(pl);
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));

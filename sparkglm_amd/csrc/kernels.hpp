@@ -53,6 +53,7 @@ int wide_panels(int p);
 int64_t wide_stride();
 // ov: the overlapped-chunk variant (wide_rows_ov_kernel: <= 96 VGPRs, fits beside the Gram kernels)
 hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st, bool ov = false);
+hipError_t launch_proc_gen(const ProcGenArgs& a, int grid, hipStream_t st);
 int wide_gram_wg_per_cu(bool diag);
 hipError_t launch_wide_gram(const WideGramArgs& a, bool diag, int grid, hipStream_t st);
 hipError_t launch_wide_reduce(const double* part, int64_t stride, const int* st_range, int p, const double* rowpart,

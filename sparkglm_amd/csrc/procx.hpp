@@ -30,6 +30,16 @@ __device__ __forceinline__ double gen_x(int kind, uint64_t kx, uint64_t gi, int 
   return kind == 3 ? (0.5 + u) * scale : (2.0 * u - 1.0) * scale;
 }
 
+// gen_x for one row, the design kind fixed at compile time (POS: kind 3): kb = kx + gi * p, the
+// row's key base (unsigned wrap-around, so kb + j is gen_x's key bit for bit).
+template <bool POS>
+__device__ __forceinline__ double gen_x_row(uint64_t kb, int j, double scale) {
+#pragma clang fp contract(off)
+  if (j == 0) return 1.0;
+  const double u = unif(kb + (uint64_t)j);
+  return POS ? (0.5 + u) * scale : (2.0 * u - 1.0) * scale;
+}
+
 // X[row, col] of a procedural shard: zero past p and on the padding rows (>= n), exactly as
 // the resident, zero-padded image.
 __device__ __forceinline__ double proc_x(const ProcX& g, int64_t row, int col) {

@@ -396,6 +396,9 @@ __device__ __forceinline__ void wide_rows_body(const WideRowArgs& a) {
           }
         }
       }
+    } else if (a.mode == MODE_IRLS && a.eta_in) {  // procedural chunk, X beta from proc_gen_kernel
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) eta[r] = (i + r < a.n) ? a.eta_in[i + r] : 0.0;
     } else if (a.mode == MODE_IRLS) {
       double e[RPT][4] = {};
       if (a.proc.on) {  // procedural design: same partial-sum order as the resident image
@@ -498,6 +501,73 @@ template <int FAM, int LNK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) wide_rows_ov_kernel(WideRowArgs a) {
   if (a.xs_out) __builtin_amdgcn_s_setprio(1);
   wide_rows_body<FAM, LNK, 2, true>(a);
+}
+
+// Procedural chunks, the generator on its own (engine.cpp, SGLM_PROC_LEAN): X rows [r_begin, r_end)
+// into the scratch and X beta into eta_raw, a thread per row, nothing else -- so that it fits in 48
+// VGPRs and two waves per SIMD run beside the two 208-VGPR off-diagonal Gram workgroups (the
+// generating wide_rows_ov_kernel, with the family arithmetic in it, holds 87 VGPRs: one wave).  The
+// family stage then runs from eta_raw (WideRowArgs::eta_in).  Partial sums in the resident order:
+// whole column quads into e[j & 3], the tail columns into e[0] (wide_rows_body), so eta is bitwise.
+// beta and the scratch are __restrict__ kernel arguments and the row loop has a uniform trip count:
+// beta is then read through the scalar cache, not by vector loads, whose vmcnt wait would also wait
+// for every scratch store in flight.  GUARD: the workgroup's rows reach past the chunk or past n.
+template <bool POS, bool GUARD>
+__device__ __forceinline__ void proc_gen_row(const ProcGenArgs& a, const double* __restrict__ beta,
+                                             double* __restrict__ xs, int64_t t) {
+  const int p = a.proc.p, pt = p & ~3;
+  const double scale = a.proc.scale;
+  const int64_t row = a.r_begin + t, ld = a.xs_ld;
+  const bool in = !GUARD || t < a.r_end - a.r_begin, valid = !GUARD || row < a.proc.n;
+  const uint64_t kb = a.proc.kx + (uint64_t)(a.proc.row0 + row) * (uint64_t)p;
+  auto gx = [&](int j) {
+    const double x = gen_x_row<POS>(kb, j, scale);
+    return valid ? x : 0.0;
+  };
+  double* xo = xs + t;
+  double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
+  int j = 0;
+  for (; j < pt; j += 4) {  // two columns at a time (two hash chains in flight: the VGPR budget)
+    const double x0 = gx(j), x1 = gx(j + 1);
+    if (in) {
+      xo[(int64_t)j * ld] = x0;
+      xo[(int64_t)(j + 1) * ld] = x1;
+    }
+    if (beta) {
+      e0 += x0 * beta[j];
+      e1 += x1 * beta[j + 1];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const double x2 = gx(j + 2), x3 = gx(j + 3);
+    if (in) {
+      xo[(int64_t)(j + 2) * ld] = x2;
+      xo[(int64_t)(j + 3) * ld] = x3;
+    }
+    if (beta) {
+      e2 += x2 * beta[j + 2];
+      e3 += x3 * beta[j + 3];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (; j < p; ++j) {
+    const double x = gx(j);
+    if (in) xo[(int64_t)j * ld] = x;
+    if (beta) e0 += x * beta[j];
+  }
+  if (beta && in && valid) a.eta_raw[row] = (e0 + e1) + (e2 + e3);
+}
+
+template <bool POS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+proc_gen_kernel(ProcGenArgs a, const double* __restrict__ beta, double* __restrict__ xs) {
+  __builtin_amdgcn_s_setprio(1);
+  const int64_t nr = a.r_end - a.r_begin;
+  for (int64_t t0 = blockIdx.x * (int64_t)blockDim.x; t0 < nr; t0 += (int64_t)gridDim.x * blockDim.x) {
+    if (t0 + (int64_t)blockDim.x <= nr && a.r_begin + t0 + (int64_t)blockDim.x <= a.proc.n)
+      proc_gen_row<POS, false>(a, beta, xs, t0 + threadIdx.x);
+    else
+      proc_gen_row<POS, true>(a, beta, xs, t0 + threadIdx.x);
+  }
 }
 
 // Packed output: lower-tri X'WX row-major | X'Wz | NS scalars, summed in a fixed order.
@@ -633,6 +703,14 @@ hipError_t launch_wide_rows(const WideRowArgs& a, int grid, hipStream_t st, bool
   const int lnk = (a.mode == MODE_LM_GRAM) ? LNK_IDENTITY : a.link;
   return ov ? launch_rows_fl<wide_rows_ov_kernel_t>(fam, lnk, g, b, st, a)
             : launch_rows_fl<wide_rows_kernel_t>(fam, lnk, g, b, st, a);
+}
+
+hipError_t launch_proc_gen(const ProcGenArgs& a, int grid, hipStream_t st) {
+  if (a.proc.kind == 3)
+    hipLaunchKernelGGL(proc_gen_kernel<true>, dim3(grid), dim3(256), 0, st, a, a.beta, a.xs);
+  else
+    hipLaunchKernelGGL(proc_gen_kernel<false>, dim3(grid), dim3(256), 0, st, a, a.beta, a.xs);
+  return hipGetLastError();
 }
 
 int wide_gram_wg_per_cu(bool diag) { return diag ? DIAG_WG : 2; }

@@ -56,3 +56,13 @@ def test_overlap_register_budget():
     for gram in (off, diag):
         assert gram["private_segment_fixed_size"] == 0
         assert 2 * _alloc(gram["vgpr_count"]) + worst_row <= 512, (gram, worst_row)
+
+
+def test_lean_generator_fits_two_waves_beside_the_gram():
+    # proc_gen_kernel (SGLM_PROC_LEAN) runs beside the off-diagonal launch: two of its waves and the
+    # two Gram waves of a SIMD must fit the 512 VGPRs together
+    meta = _kernel_meta()
+    off = meta["_ZN4sglm16wide_gram_kernelILb0ELb0EEEvNS_12WideGramArgsE"]
+    gen = meta["_ZN4sglm15proc_gen_kernelILb0EEEvNS_11ProcGenArgsEPKdPd"]
+    assert gen["private_segment_fixed_size"] == 0
+    assert 2 * _alloc(off["vgpr_count"]) + 2 * _alloc(gen["vgpr_count"]) <= 512, (off, gen)

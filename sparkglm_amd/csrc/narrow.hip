@@ -119,7 +119,7 @@ __device__ __forceinline__ double xor32_sum(double v) {
 // (4 x NRB doubles on 2 NRB lanes).  Column groups past the stored columns re-load the last
 // stored group (finite data; beta is 0 and the tiles are discarded past p), so every block
 // issues exactly NOCT + 1 vector-memory operations.
-template <int P16>
+template <int P16, int AUX>
 __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, int64_t blk, int ngrp_stored,
                                        const int64_t (&loff)[NGeo<P16>::LPER], const double* vsrc, int lane) {
   using G = NGeo<P16>;
@@ -129,10 +129,10 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
   for (int o = 0; o < G::NOCT; ++o) {
     const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
     __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER]),
-                                     (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16, 0, DMA_NT);
+                                     (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16, 0, AUX);
   }
   if (G::NRB == 32 || lane < 2 * G::NRB)
-    __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, DMA_NT);
+    __builtin_amdgcn_global_load_lds((const void*)(vsrc + blk * G::NRB), (lds_void*)(dst + G::XB), 16, 0, AUX);
 }
 
 // Lane l of a 16-lane row takes the value of lane l & ~12 (the first 4-lane group's lane of the same
@@ -255,9 +255,14 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   const int cl = lane & 15, rq = lane >> 4;
   const int fcl = swz<NRB>(cl);  // f(16b + cl) does not depend on b
   const bool do_gram = !a.no_gram;
+  // Cache policy of the design stream: non-temporal in the IRLS passes (a large shard streamed once
+  // per pass), the default in the LM Gram pass and the initial pass, whose X the next pass re-reads --
+  // at configs[0]'s 1M x 20 (160 MB) the LM residual pass finds it in the Infinity Cache (31.3 us
+  // against 36.7 us after a non-temporal Gram pass)
+  constexpr int DAUX = IRLS ? DMA_NT : 0;  // (spelled out in stage_next)
 
-  if (b0 < b1) nstage<P16>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
-  if (b0 + 1 < b1) nstage<P16>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
+  if (b0 < b1) nstage<P16, DAUX>(wl, 0, a, b0, ngrp_stored, loff, vsrc, lane);
+  if (b0 + 1 < b1) nstage<P16, DAUX>(wl, 1, a, b0 + 1, ngrp_stored, loff, vsrc, lane);
 
   // The blocks alternate the two buffers, so the loops take them in pairs with the buffer a
   // compile-time constant: every LDS address is a per-lane base fixed for the kernel plus an immediate
@@ -295,11 +300,11 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     for (int o = 0; o < G::NOCT; ++o) {
       if (o > 0 && o < ngrp_stored) co += cs;  // uniform: groups past the stored columns repeat the last
       __builtin_amdgcn_global_load_lds((const void*)(dsrc[o % G::LPER] + co),
-                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, DMA_NT);
+                                       (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, IRLS ? DMA_NT : 0);
     }
 #pragma unroll
     for (int o = 0; o < G::LPER; ++o) dsrc[o] += NRB;
-    if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, DMA_NT);
+    if (G::NRB == 32 || lane < 2 * NRB) __builtin_amdgcn_global_load_lds((const void*)vnext, (lds_void*)(dst + G::XB), 16, 0, IRLS ? DMA_NT : 0);
     vnext += NRB;
   };
   // eta: every LDS read of the row's columns issued before the first FMA (the scheduler had

@@ -13,7 +13,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-WIDE = ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel"]
+WIDE = ["wide_rows_kernel", "wide_rows_ov_kernel", "wide_gram_kernel", "proc_gen_kernel"]
 WL = {  # name: (key, rows, kernel substrings of the pass, substring of the kernel dispatched once per pass)
     "logit32": ("binomial:32", 100_000_000, ["irls_narrow_kernel"], "irls_narrow_kernel"),
     "poisson64": ("poisson:64", 50_000_000, ["irls_narrow_kernel"], "irls_narrow_kernel"),

@@ -75,8 +75,38 @@ WORKLOADS = {
 }
 
 
-def cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
-    """The CPU restatement (oracle/, test infrastructure) timed on a bounded sample."""
+def host_cores(env=None) -> dict:
+    """The host cores the CPU baseline runs on ("timed on the same box's host cores,
+    with N stated").  N = the cores this process may use: the scheduler affinity mask, capped by
+    OMP_NUM_THREADS when the environment sets it -- on the GPU pool every box is a 16-core share
+    of a larger host (OMP_NUM_THREADS=16 there; os.cpu_count() reports the whole host's CPUs, which
+    this job does not own).  The line records all three numbers."""
+    env = os.environ if env is None else env
+    total = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = total
+    try:
+        omp = int(env.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    threads = max(1, min(affinity, omp) if omp > 0 else affinity)
+    return {"threads": threads, "host_cpu_count": total, "affinity_cpus": affinity,
+            "omp_num_threads": omp or None}
+
+
+def cpu_baseline(wl: dict, p: int, rows: int, threads: int | None = None) -> dict:
+    """The CPU restatement (oracle/, test infrastructure) timed on a bounded sample, on every host
+    core this job owns (host_cores), one Spark-style partition per thread."""
+    hc = host_cores()
+    threads = threads or hc["threads"]
+    res = _cpu_baseline(wl, p, rows, threads)
+    res["host_cores"] = hc
+    return res
+
+
+def _cpu_baseline(wl: dict, p: int, rows: int, threads: int) -> dict:
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import pyoracle  # noqa: E402  (checker / CPU baseline only)
     from sparkglm_amd import synth
@@ -373,8 +403,7 @@ def main() -> int:
             "solve_path": st["solve_path_name"],
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
+            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"])
         else:
             out["cpu_baseline"] = None
     eng.close()
@@ -584,8 +613,7 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
                                       "solve": st["solve_ms"] / args.steps, "comm": st["comm_ms"] / args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"], threads)
+            out["cpu_baseline"] = cpu_baseline(wl, p, args.cpu_rows or wl["cpu_rows"])
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), file=JSON_OUT, flush=True)

@@ -25,7 +25,8 @@
  *   sglm_predict_new     replaces LM.predictSingle/predictMultiple's newX * coefs
  *                        (LM.scala:39-61) on new rows, without evicting the resident shard;
  *                        response scale (mu = unlink(eta)) for GLMs.
- *   sglm_create_multi    one process owning several GPUs (the single Spark driver that calls
+ *   sglm_create          SURVEY 8(b)'s constructor over devs[0..ndev): one device, or one
+ *                        process owning several GPUs (the single Spark driver that calls
  *                        GLM.fit / LM.fit, GLM.scala:587, LM.scala:254): row shards per device,
  *                        one RCCL group all-reduce (ncclCommInitAll) per iteration.
  *   sglm_glm_summary / sglm_lm_summary
@@ -39,8 +40,8 @@
  *   - Matrices are column-major fp64 (Breeze DenseMatrix layout): element (i,j) at
  *     X[i + j*ldx].  The caller keeps ownership of every pointer it passes; the engine
  *     copies into device memory it owns until sglm_destroy.
- *   - A handle from sglm_create drives one HIP device; one from sglm_create_multi drives
- *     several (row shards, Spark's slicing [d n/D, (d+1) n/D)).  Across processes (or host
+ *   - A handle from sglm_create with ndev = 1 (or sglm_create_device) drives one HIP device;
+ *     with ndev > 1 it drives several (row shards, Spark's slicing [d n/D, (d+1) n/D)).  Across processes (or host
  *     threads, one handle each) shards join a communicator: RCCL over xGMI, a caller-supplied
  *     all-reduce, or the in-process sglm_local_allreduce.  Every rank receives identical results.
  *   - Handles are not thread-safe; distinct handles may be used concurrently.
@@ -55,11 +56,13 @@
 extern "C" {
 #endif
 
-#define SGLM_ABI_VERSION 7  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
+#define SGLM_ABI_VERSION 8  /* 3: sglm_stats.dev_passes; 4: sglm_stats.overlap_chunks; 5: sglm_set_comm_rank,
                               sglm_stats.comm_path / rank_blocks / pass_kernel_ms_min / proc_chunks /
                               proc_chunk_rows / solve_path; 6: sglm_stats.pass_kernel / pass_kernel_name,
                               sglm_set_comm_rank collective; 7: sglm_stats.lm_device_fits /
-                              lm_device_reruns */
+                              lm_device_reruns; 8: sglm_create(devs, ndev) as SURVEY 8(b) names it
+                              (was sglm_create_multi), the one-device form renamed sglm_create_device,
+                              SGLM_KERNEL_NARROW_SPLIT retired */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -110,9 +113,8 @@ enum sglm_pass_kernel {
   SGLM_KERNEL_FUSED_SPLIT = 2, /* irls_pass_r_kernel<P16, fam, link> (K1r, split roles) */
   SGLM_KERNEL_NARROW = 3,      /* irls_narrow_kernel<P16, fam, link, irls, stats>: p <= 64 */
   SGLM_KERNEL_WIDE = 4,        /* wide_rows_kernel + wide_gram_kernel: p > 256 (resident X) */
-  SGLM_KERNEL_WIDE_PROC = 5,   /* the same over procedural X (generated chunks or in-kernel) */
-  SGLM_KERNEL_NARROW_SPLIT = 6 /* irls_narrow_r_kernel<P16, fam, link, irls, stats>: split-role narrow pass,
-                                  33 <= p <= 64 by default (SGLM_NARROW_SPLIT) */
+  SGLM_KERNEL_WIDE_PROC = 5    /* the same over procedural X (generated chunks or in-kernel) */
+  /* 6 (SGLM_KERNEL_NARROW_SPLIT, ABI <= 7): retired with its kernel, never returned */
 };
 
 /* Prediction scale (R's predict(type = "link" | "response")). */
@@ -202,20 +204,29 @@ typedef struct {
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
- * pointer and stream the engine's hipStream_t; otherwise buf is host memory. */
+ * pointer and stream the engine's hipStream_t; otherwise buf is host memory.
+ * THREAD: with a deadline (SGLM_COMM_TIMEOUT_S > 0, the default 300 s, read when the communicator
+ * is set) the callback runs on a communicator thread the handle owns (its device current), not on
+ * the thread that called sglm_fit_* / sglm_irls_*, which waits with the deadline; a callback still
+ * running at the deadline is abandoned on that thread.  Callbacks bound to the calling thread
+ * (MPI_THREAD_SINGLE / FUNNELED, thread-local JNI or torch state) need SGLM_COMM_TIMEOUT_S=0: the
+ * callback then runs inline on the caller's thread, without a deadline.  sglm_local_allreduce
+ * always runs inline (it bounds its own wait). */
 typedef int (*sglm_allreduce_fn)(void *ctx, double *buf, int64_t count, void *stream, int on_device);
 
 /* ---- lifecycle ---------------------------------------------------------------- */
 int sglm_abi_version(void);
 const char *sglm_last_error(void);
 int sglm_device_count(int *count);
-int sglm_create(int device, sglm_engine **out);
-/* One handle over devs[0..ndev): rows are sharded contiguously across the devices; each
+/* One handle over devs[0..ndev).  ndev = 1: a single-device handle, exactly
+ * sglm_create_device(devs[0]).  ndev > 1: rows are sharded contiguously across the devices; each
  * iteration's packed partials are all-reduced by one RCCL group call over communicators from
  * ncclCommInitAll (distinct devices) or summed on the host in device order (a device listed
- * twice: rehearsal on fewer GPUs).  Every call below accepts it, except sglm_set_data_device,
- * sglm_set_comm and sglm_set_comm_rccl. */
-int sglm_create_multi(const int *devs, int ndev, sglm_engine **out);
+ * twice: rehearsal on fewer GPUs).  Every call below accepts a multi-device handle, except
+ * sglm_set_data_device, sglm_set_comm and sglm_set_comm_rccl. */
+int sglm_create(const int *devs, int ndev, sglm_engine **out);
+/* One device by ordinal (the ABI <= 7 sglm_create(int, ...)). */
+int sglm_create_device(int device, sglm_engine **out);
 int sglm_handle_devices(sglm_engine *h, int *ndev);
 void sglm_destroy(sglm_engine *h);
 
@@ -252,6 +263,9 @@ int sglm_synth_procedural(sglm_engine *h, int kind, int64_t row0, int64_t n, int
 int sglm_get_data(sglm_engine *h, double *X, double *y, double *m, double *offset, double *prior);
 
 /* ---- communicators (Spark treeReduce replacement) ----------------------------- */
+/* fn runs on the handle's communicator thread unless SGLM_COMM_TIMEOUT_S=0 (see sglm_allreduce_fn).
+ * RCCL (sglm_set_comm_rccl) and group handles: the deadline of each pass's all-reduce starts when
+ * this rank's own pass kernels have finished, so it bounds the wait for the peers only. */
 int sglm_set_comm(sglm_engine *h, sglm_allreduce_fn fn, void *ctx, int on_device);
 /* This handle's rank in the communicator just set by sglm_set_comm (0 <= rank < its rank count;
  * known without this call for RCCL and sglm_local_allreduce).  With it the per-iteration scalars
@@ -305,8 +319,7 @@ int sglm_get_stats(sglm_engine *h, sglm_stats *out);
 /* The kernel an engine would run a pass of an n x p shard with (enum sglm_pass_kernel, -1 on bad
  * arguments) and its name into name[namelen] -- the engine's own dispatch rule, for callers and CPU
  * tests.  fused_split: SGLM_FUSED_SPLIT's meaning (1 default threshold, 0 never K1r, N from P16 = N);
- * flags: 1 procedural shard, 2 forced wide path (SGLM_FORCE_WIDE), bits 4..7 SGLM_NARROW_SPLIT + 1 (0: the
- * default threshold).  No device is touched. */
+ * flags: 1 procedural shard, 2 forced wide path (SGLM_FORCE_WIDE).  No device is touched. */
 int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int family, int link, char *name,
                          int64_t namelen);
 int sglm_reset_stats(sglm_engine *h);
@@ -323,6 +336,7 @@ typedef struct {
   int (*pass)(void *ctx, int mode, const double *beta, double mu0, double ybar, double *packed);
 } sglm_backend;
 
+/* fn: as sglm_set_comm's (the communicator thread unless SGLM_COMM_TIMEOUT_S=0). */
 int sglm_fit_glm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *comm_ctx,
                           const sglm_glm_opts *opts, sglm_preglm *out);
 int sglm_fit_lm_external(const sglm_backend *be, sglm_allreduce_fn fn, void *comm_ctx,

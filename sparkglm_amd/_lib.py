@@ -29,7 +29,7 @@ EXPORTS = [
     "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
     "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
-    "sglm_pval_normal", "sglm_pval_t", "sglm_create_multi", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
+    "sglm_pval_normal", "sglm_pval_t", "sglm_create_device", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
     "sglm_predict_glm", "sglm_predict_new", "sglm_local_comm_create", "sglm_local_comm_destroy",
     "sglm_local_comm_rank", "sglm_local_allreduce", "sglm_set_comm_rank", "sglm_pass_kernel_for",
 ]
@@ -69,8 +69,7 @@ class Stats(C.Structure):
 
 COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}
 SOLVE_PATHS = {-1: "none", 0: "host-cholesky", 1: "host-lu", 2: "device-cholesky", 3: "device-lu"}
-PASS_KERNELS = {0: "none", 1: "fused", 2: "fused-split", 3: "narrow", 4: "wide", 5: "wide-procedural",
-                6: "narrow-split"}
+PASS_KERNELS = {0: "none", 1: "fused", 2: "fused-split", 3: "narrow", 4: "wide", 5: "wide-procedural"}
 
 
 class GlmDerived(C.Structure):
@@ -124,7 +123,8 @@ def load():
         "sglm_abi_version": ([], C.c_int),
         "sglm_last_error": ([], C.c_char_p),
         "sglm_device_count": ([C.POINTER(C.c_int)], C.c_int),
-        "sglm_create": ([C.c_int, E], C.c_int),
+        "sglm_create": ([C.POINTER(C.c_int), C.c_int, E], C.c_int),
+        "sglm_create_device": ([C.c_int, E], C.c_int),
         "sglm_destroy": ([h], None),
         "sglm_set_data": ([h, dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, dp], C.c_int),
         "sglm_set_data_device": ([h, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
@@ -157,7 +157,6 @@ def load():
         "sglm_java_double_string": ([C.c_double, C.c_char_p, C.c_int64], C.c_int64),
         "sglm_pval_normal": ([C.c_double], C.c_double),
         "sglm_pval_t": ([C.c_double, C.c_double], C.c_double),
-        "sglm_create_multi": ([C.POINTER(C.c_int), C.c_int, E], C.c_int),
         "sglm_handle_devices": ([h, C.POINTER(C.c_int)], C.c_int),
         "sglm_reserve": ([h, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int], C.c_int),
         "sglm_set_rows": ([h, C.c_int64, C.c_int64, dp, C.c_int64, dp, dp, dp, dp], C.c_int),
@@ -182,11 +181,10 @@ def load():
 
 
 def pass_kernel_for(n: int, p: int, family: str = "binomial", link: str = "logit", fused_split: int = 1,
-                    procedural: bool = False, force_wide: bool = False, narrow_split=None):
-    """(kind, name) of the kernel an engine runs an n x p pass with (sglm_pass_kernel_for; no GPU).
-    narrow_split: SGLM_NARROW_SPLIT's meaning (None: the default threshold, 0 never, N from P16 = N)."""
+                    procedural: bool = False, force_wide: bool = False):
+    """(kind, name) of the kernel an engine runs an n x p pass with (sglm_pass_kernel_for; no GPU)."""
     buf = C.create_string_buffer(64)
-    flags = (1 if procedural else 0) | (2 if force_wide else 0) | ((0 if narrow_split is None else int(narrow_split) + 1) << 4)
+    flags = (1 if procedural else 0) | (2 if force_wide else 0)
     k = load().sglm_pass_kernel_for(int(n), int(p), int(fused_split), flags, FAMILIES[family], LINKS[link], buf, 64)
     if k < 0:
         raise IllegalArgumentException(last_error())

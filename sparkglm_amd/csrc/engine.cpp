@@ -84,9 +84,20 @@ std::string rank_str(int rank) { return rank >= 0 ? "rank " + std::to_string(ran
 // communicator, or a multi-device handle's ncclCommInitAll group): poll hipStreamQuery and every
 // communicator's asynchronous error until the streams drain or the deadline passes.  On a remote
 // error or expiry the communicators are aborted (ncclCommAbort makes their kernels exit) and
-// nulled, and SGLM_ECOMM is returned -- never a silent hang.
+// nulled, and SGLM_ECOMM is returned -- never a silent hang.  `starts`: events recorded on those
+// streams just before the collective (this rank's own pass done); the deadline counts from the
+// moment all of them have completed, so it bounds the wait for the peers, never this rank's own
+// pass kernels (a long pass on a large shard cannot expire it).
 int wait_collective(const std::vector<hipStream_t>& sts, std::vector<ncclComm_t*> comms, double timeout_ms,
-                    int rank, const char* what) {
+                    int rank, const char* what, const std::vector<hipEvent_t>& starts = {}) {
+  for (hipEvent_t ev : starts) {  // this rank's pass kernels: no deadline (they need no peer)
+    hipError_t e;
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::yield();
+    if (e != hipSuccess) {
+      set_error(hip_msg(e, "hipEventQuery (the pass before the all-reduce)"));
+      return SGLM_EHIP;
+    }
+  }
   const double t0 = now_ms();
   std::vector<char> done(sts.size(), 0);
   size_t left = sts.size();
@@ -309,14 +320,8 @@ void pack_cols(double* dst, const double* src, int64_t sld, int64_t rows, int64_
 // ensure_workspace / launch_pass / launch_narrow / the wide path, in one place (the engine labels
 // its passes with it; sglm_pass_kernel_for exposes it for a CPU test of the mapping).
 namespace {
-// SGLM_NARROW_SPLIT: narrow shards of P16 >= this many column blocks run the split-role narrow pass
-// (irls_narrow_r_kernel, narrow_r.hip); 0 never (the default: measured slower, DESIGN.md 4 K1'r).
-constexpr int NARROW_SPLIT_DEFAULT = 0;
-bool narrow_uses_split(int P16, int narrow_split, int64_t n_pad) {
-  return narrow_split > 0 && P16 >= narrow_split && narrow_r_ok(P16, n_pad);
-}
-int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc, int fused_split, int narrow_split,
-                       int family, int link, char* name, size_t len) {
+int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc, int fused_split, int family,
+                       int link, char* name, size_t len) {
   static const char* fam[] = {"binomial", "gaussian", "poisson", "gamma"};
   static const char* lnk[] = {"logit", "probit", "cloglog", "identity", "log", "inverse"};
   const char* f = (family >= 0 && family < 4) ? fam[family] : "?";
@@ -325,9 +330,6 @@ int pass_kernel_choice(int64_t n_pad, int P16, bool narrow, bool wide, bool proc
   if (wide) {
     k = proc ? SGLM_KERNEL_WIDE_PROC : SGLM_KERNEL_WIDE;
     std::snprintf(name, len, "wide_gram_kernel<%s>", proc ? "procedural" : "resident");
-  } else if (narrow && narrow_uses_split(P16, narrow_split, n_pad)) {
-    k = SGLM_KERNEL_NARROW_SPLIT;
-    std::snprintf(name, len, "irls_narrow_r_kernel<%d,%s,%s>", P16, f, l);
   } else if (narrow) {
     k = SGLM_KERNEL_NARROW;
     std::snprintf(name, len, "irls_narrow_kernel<%d,%s,%s>", P16, f, l);
@@ -355,6 +357,7 @@ struct sglm_local_comm {
   int64_t count = -1;
   bool failed = false;  // this round: a rank passed another count
   bool result = false;  // the last completed round failed (read by its waiters only)
+  double timeout_ms = 0.0;  // SGLM_COMM_TIMEOUT_S, read once by sglm_local_comm_create
   struct Rank {
     sglm_local_comm* c;
     int rank;
@@ -396,10 +399,8 @@ struct sglm_engine : public Backend {
   bool dev_only = false, allow_spec = true;
   // wide path (wide.hip)
   bool wide = false, force_wide = false;
-  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines; narrow_r: its split-role
-  // form (narrow_r.hip) for P16 >= narrow_split (SGLM_NARROW_SPLIT, 0 never)
-  bool narrow = false, narrow_r = false;
-  int narrow_split = NARROW_SPLIT_DEFAULT;
+  // narrow path (narrow.hip, p <= 64): barrier-free per-wave pipelines
+  bool narrow = false;
   // procedural shard (sglm_synth_procedural): X regenerated in the wide kernels, not stored
   ProcX procx{};
   // procedural shards in chunks (setup_proc_chunks): each pass generates C rows of X at a time
@@ -408,7 +409,6 @@ struct sglm_engine : public Backend {
   int64_t ch_rows = 0;  // rows per chunk (multiple of 32); 0: in-kernel generation (PROC kernels)
   int nch = 0;
   std::vector<hipEvent_t> evch;  // [4 * nch + 1]: row span, Gram span per chunk; st -> st2 fork
-  std::vector<hipEvent_t> evdg;  // [nch]: chunk c's diagonal launch done (SGLM_PROC_OV_GATE)
   double *dxsc = nullptr, *dchunks = nullptr;
   bool allow_chunks = true;  // SGLM_PROC_CHUNKS=0 disables
   // SGLM_PROC_OVERLAP: chunks of an overlapped procedural pass (<= 1: one buffer, serial).  Round 2
@@ -416,12 +416,11 @@ struct sglm_engine : public Backend {
   // 1480 at 8 / 16 chunks -- the generator's integer + fp64 VALU slowed the Gram by 31-38 %).  Round 5
   // (VERDICT r4 item 6): gated to the off-diagonal launches (SGLM_PROC_OV_GATE; the diagonal launch
   // goes first) and the generating row kernel at raised priority, 8 chunks: 1284.5 -> 1266.9 ms on one
-  // box (ungated 1466.3, gated at normal priority 1285.7).
+  // box (ungated 1466.3, gated at normal priority 1285.7).  Round 5 then split the
+  // generator off (proc_gen_kernel, 48 VGPRs) and let it start beside each chunk's diagonal launch,
+  // which goes first; round 6 measured the other launch orders +4.5 % (generator held until the
+  // diagonal launch is done) and +5.5 % (off-diagonal launch first) and retired them.
   int proc_ov_want = 8;
-  // SGLM_PROC_OV_GATE: the diagonal launch of every chunk first (1, 2; 0: off-diagonal first), and
-  // (1) the row kernel of chunk c + 1 held until chunk c's diagonal launch is done
-  int proc_ov_gate = 2;
-  int proc_lean = 1;  // SGLM_PROC_LEAN: chunks >= 1 generate in proc_gen_kernel (1), chunk 0 too (2), off (0)
   bool proc_ov = false;      // double-buffered scratch, row kernels on st2 (as the resident overlap below)
   int64_t proc_ov_min = (int64_t)1 << 20;  // SGLM_PROC_OV_MIN: fewest rows per overlapped chunk
   // resident wide shards, overlapped passes: the rows are cut into nov chunks; the row kernel of
@@ -536,8 +535,6 @@ struct sglm_engine : public Backend {
     comm.nccl = nullptr;
     for (hipEvent_t e : evch) (void)hipEventDestroy(e);
     evch.clear();
-    for (hipEvent_t e : evdg) (void)hipEventDestroy(e);
-    evdg.clear();
     for (hipEvent_t e : evov) (void)hipEventDestroy(e);
     evov.clear();
     if (st2) (void)hipStreamDestroy(st2);
@@ -588,7 +585,10 @@ struct sglm_engine : public Backend {
         return SGLM_ECOMM;
       }
       if (after_pass) HIPCHK(hipEventRecord(evc, st));
-      if (int rc = wait_collective({st}, {&comm.nccl}, comm.timeout_ms, comm.rank, "ncclAllReduce")) return rc;
+      // after a pass: the deadline starts when the pass (ev2, recorded before the collective) is done
+      if (int rc = wait_collective({st}, {&comm.nccl}, comm.timeout_ms, comm.rank, "ncclAllReduce",
+                                   after_pass ? std::vector<hipEvent_t>{ev2} : std::vector<hipEvent_t>{}))
+        return rc;
       if (after_pass) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, ev2, evc));
@@ -893,11 +893,6 @@ struct sglm_engine : public Backend {
       HIPCHK(hipEventCreate(&e));
       evch.push_back(e);
     }
-    while (evdg.size() < (size_t)nch) {
-      hipEvent_t e = nullptr;
-      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      evdg.push_back(e);
-    }
     HIPCHK(hipStreamSynchronize(st));
     return ensure_wide_workspace();  // the Gram schedule for ch_rows-row chunks
   }
@@ -909,13 +904,11 @@ struct sglm_engine : public Backend {
       if (rc) return rc;
     }
     narrow = !wide && p <= 64;
-    narrow_r = false;
     if (narrow) {
       P16 = narrow_variant((int)p);
       stride = narrow_stride(P16);
-      narrow_r = narrow_uses_split(P16, narrow_split, n_pad);
-      const int64_t want_grid = (int64_t)ncu * (narrow_r ? 1 : narrow_wg_per_cu());
-      const int64_t per_wg = narrow_r ? NARROW_R_ROWS : narrow_rows_per_wg(P16);
+      const int64_t want_grid = (int64_t)ncu * narrow_wg_per_cu();
+      const int64_t per_wg = narrow_rows_per_wg(P16);
       const int64_t need = (nblocks * RB + per_wg - 1) / per_wg;
       grid = (int)std::max<int64_t>(1, std::min(need, want_grid));
     } else {
@@ -1370,13 +1363,11 @@ struct sglm_engine : public Backend {
           r.r_end = r.r_begin + ch_rows;
           r.xs_out = dev_only ? nullptr : xs;  // deviance only: eta from the generator, no scratch
           r.row_partials = proc_ov ? rowpart(c) : drp;
-          // buffer c & 1 is free once the Gram kernels of chunk c - 2 are done with it
+          // buffer c & 1 is free once the Gram kernels of chunk c - 2 are done with it: chunk c's
+          // generator then starts beside chunk c - 1's diagonal launch (which goes first, below)
           if (proc_ov && c >= 2) HIPCHK(hipStreamWaitEvent(st2, evch[(size_t)4 * (c - 2) + 3], 0));
-          // gated: the row kernel of chunk c starts once chunk c - 1's diagonal launch is done, so it
-          // runs beside that chunk's off-diagonal launch only (the diagonal launch goes first)
-          if (proc_ov && proc_ov_gate == 1 && c >= 1) HIPCHK(hipStreamWaitEvent(st2, evdg[(size_t)c - 1], 0));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c], rs));
-          if (!dev_only && proc_ov && proc_lean > (c > 0 ? 0 : 1)) {
+          if (!dev_only && proc_ov && c > 0) {
             // the lean generator (X into the scratch, X beta into deta), then the family stage from deta
             ProcGenArgs pg{};
             pg.proc = procx;
@@ -1401,17 +1392,14 @@ struct sglm_engine : public Backend {
           g.X = xs;
           g.w = dw + r.r_begin;
           g.wz = dwz + r.r_begin;
-          const bool gate = proc_ov && proc_ov_gate;
           for (int q = 0; q < 2 && !dev_only; ++q) {
-            const int kind = gate ? 1 - q : q;  // gated: diagonal first
+            const int kind = proc_ov ? 1 - q : q;  // overlapped: the diagonal launch first
             if (has_sched[kind]) {
               g.pieces = dpieces[kind];
               g.wg_begin = dwgb[kind];
               HIPCHK(launch_wide_gram(g, kind == 1, ggk[kind], st));
             }
-            if (gate && kind == 1) HIPCHK(hipEventRecord(evdg[(size_t)c], st));
           }
-          if (gate && dev_only) HIPCHK(hipEventRecord(evdg[(size_t)c], st));
           HIPCHK(hipEventRecord(evch[(size_t)4 * c + 3], st));
           HIPCHK(launch_wide_reduce(dgp, wstride, dstr, (int)p, r.row_partials, proc_ov && c > 0 ? rgrid_ov : rgrid,
                                     dchunks + (int64_t)c * plen, st));
@@ -1477,8 +1465,7 @@ struct sglm_engine : public Backend {
       // a tenth of an LM.fit on configs[0]
       hipEvent_t e0 = timed ? ev0 : nullptr, e1 = timed ? ev1 : nullptr, e2 = timed ? ev2 : nullptr;
       if (nblocks > 0) {
-        if (narrow_r) HIPCHK(launch_narrow_r(P16, a, grid, st, e0, e1));
-        else if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, e0, e1));
+        if (narrow) HIPCHK(launch_narrow(P16, a, grid, st, e0, e1));
         else HIPCHK(launch_pass(P16, a, grid, st, e0, e1));
       } else {
         HIPCHK(hipEventRecord(ev0, st));
@@ -1497,7 +1484,7 @@ struct sglm_engine : public Backend {
   // own dispatch decision -- narrow / fused / wide, and K1 against K1r by pass_uses_split with its
   // row limit -- so a roofline line is labelled by what ran, not by a re-derived threshold.
   void note_kernel(int family, int link) {
-    last_kernel = pass_kernel_choice(n_pad, P16, narrow, wide, procx.on != 0, fused_split, narrow_split, family, link,
+    last_kernel = pass_kernel_choice(n_pad, P16, narrow, wide, procx.on != 0, fused_split, family, link,
                                      last_kernel_name, sizeof last_kernel_name);
   }
 
@@ -1545,11 +1532,13 @@ struct sglm_engine : public Backend {
       {  // every shard's stream drains, or the group is aborted at the deadline (wait_collective)
         std::vector<hipStream_t> sts;
         std::vector<ncclComm_t*> cs;
+        std::vector<hipEvent_t> evs;  // every shard's pass done: the deadline starts there
         for (int d = 0; d < D; ++d) {
           sts.push_back(subs[d]->st);
           cs.push_back(&gcomms[d]);
+          evs.push_back(subs[d]->ev2);
         }
-        if (int rc = wait_collective(sts, cs, comm.timeout_ms, -1, "the multi-device ncclAllReduce group")) {
+        if (int rc = wait_collective(sts, cs, comm.timeout_ms, -1, "the multi-device ncclAllReduce group", evs)) {
           group_aborted = true;  // the handle's communicators are gone: every later pass fails
           return rc;
         }
@@ -1990,7 +1979,7 @@ int sglm_device_count(int* count) {
   return SGLM_OK;
 }
 
-int sglm_create(int device, sglm_engine** out) {
+int sglm_create_device(int device, sglm_engine** out) {
   if (!out) {
     set_error("requirement failed: out handle pointer");
     return SGLM_EINVAL;
@@ -2025,15 +2014,12 @@ int sglm_create(int device, sglm_engine** out) {
   if (const char* fw = std::getenv("SGLM_FORCE_WIDE")) h->force_wide = std::atoi(fw) != 0;
   if (const char* pc = std::getenv("SGLM_PROC_CHUNKS")) h->allow_chunks = std::atoi(pc) != 0;
   if (const char* po = std::getenv("SGLM_PROC_OVERLAP")) h->proc_ov_want = std::atoi(po);
-  if (const char* pg = std::getenv("SGLM_PROC_OV_GATE")) h->proc_ov_gate = std::atoi(pg);
-  if (const char* pl = std::getenv("SGLM_PROC_LEAN")) h->proc_lean = std::atoi(pl);
   if (const char* pm = std::getenv("SGLM_PROC_OV_MIN")) h->proc_ov_min = std::max<int64_t>(32, std::atoll(pm));
   if (const char* ov = std::getenv("SGLM_WIDE_OVERLAP")) h->ov_want = std::atoi(ov);
   if (const char* om = std::getenv("SGLM_WIDE_OV_MIN")) h->ov_min = std::max<int64_t>(32, std::atoll(om));
   if (const char* sp = std::getenv("SGLM_SPECULATE")) h->allow_spec = std::atoi(sp) != 0;
   if (const char* ld = std::getenv("SGLM_LM_DEVICE")) h->allow_lm_device = std::atoi(ld) != 0;
   if (const char* fs = std::getenv("SGLM_FUSED_SPLIT")) h->fused_split = std::max(0, std::atoi(fs));
-  if (const char* ns = std::getenv("SGLM_NARROW_SPLIT")) h->narrow_split = std::max(0, std::atoi(ns));
   if (const char* ws = std::getenv("SGLM_WIDE_SOLVE")) h->wide_lu = std::strcmp(ws, "lu") == 0;
   if (const char* pm = std::getenv("SGLM_PROC_SCRATCH_MAX")) h->proc_scratch_max = std::max<int64_t>(0, std::atoll(pm));
   *out = h;
@@ -2042,17 +2028,21 @@ int sglm_create(int device, sglm_engine** out) {
 
 void sglm_destroy(sglm_engine* h) { delete h; }
 
-int sglm_create_multi(const int* devs, int ndev, sglm_engine** out) {
+// SURVEY 8(b)'s constructor: one handle over devs[0..ndev).  One device: the single-device handle
+// (sglm_create_device); several: the group handle -- one shard engine per listed device, one RCCL
+// communicator per device from ncclCommInitAll when they are distinct.
+int sglm_create(const int* devs, int ndev, sglm_engine** out) {
   if (!out || !devs || ndev < 1) {
     set_error("requirement failed: devs[ndev], ndev >= 1, out handle pointer");
     return SGLM_EINVAL;
   }
   *out = nullptr;
+  if (ndev == 1) return sglm_create_device(devs[0], out);
   auto* g = new sglm_engine();
   g->device = devs[0];
   for (int d = 0; d < ndev; ++d) {
     sglm_engine* s = nullptr;
-    int rc = sglm_create(devs[d], &s);
+    int rc = sglm_create_device(devs[d], &s);
     if (rc) {
       delete g;
       return rc;
@@ -2502,11 +2492,7 @@ int sglm_pass_kernel_for(int64_t n, int64_t p, int fused_split, int flags, int f
   const bool proc = (flags & 1) != 0, wide = proc || (flags & 2) || p > 16 * MAX_P16, narrow = !wide && p <= 64;
   const int P16 = wide ? 0 : narrow ? narrow_variant((int)p) : pass_variant((int)p, fused_split, n_pad);
   char buf[64];
-  // flags bits 4..7: SGLM_NARROW_SPLIT + 1 (0: the default threshold)
-  const int ns_flag = (flags >> 4) & 15;
-  const int narrow_split = ns_flag == 0 ? NARROW_SPLIT_DEFAULT : ns_flag - 1;
-  const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, narrow_split, family, link, buf,
-                                   sizeof buf);
+  const int k = pass_kernel_choice(n_pad, P16, narrow, wide, proc, fused_split, family, link, buf, sizeof buf);
   if (name && namelen > 0) std::snprintf(name, (size_t)namelen, "%s", buf);
   return k;
 }
@@ -2617,6 +2603,7 @@ int sglm_local_comm_create(int nranks, sglm_local_comm** out) {
   }
   auto* c = new sglm_local_comm();
   c->nranks = nranks;
+  c->timeout_ms = comm_timeout_ms_env();  // once, here: no getenv on the rank threads' all-reduces
   c->bufs.assign((size_t)nranks, nullptr);
   for (int r = 0; r < nranks; ++r) c->ranks.push_back({c, r});
   *out = c;
@@ -2658,7 +2645,7 @@ int sglm_local_allreduce(void* ctx, double* buf, int64_t count, void* stream, in
   } else {
     // bounded (SGLM_COMM_TIMEOUT_S): a rank that never arrives fails the round for everyone
     // instead of leaving the others blocked; the one timing out withdraws its buffer
-    const double tmo = comm_timeout_ms_env();
+    const double tmo = c->timeout_ms;
     auto arrived = [&] { return c->generation != gen; };
     if (tmo > 0.0) {
       if (!c->cv.wait_for(lk, std::chrono::duration<double, std::milli>(tmo), arrived)) {

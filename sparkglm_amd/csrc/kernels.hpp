@@ -42,11 +42,6 @@ int narrow_wg_per_cu();
 int narrow_rows_per_wg(int P16); // rows one workgroup streams per block step (waves x rows per block)
 hipError_t launch_narrow(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0 = nullptr,
                          hipEvent_t e1 = nullptr);
-// split-role narrow path (narrow_r.hip): 17 <= p <= 64 on 64-row blocks, one 12-wave workgroup per CU
-constexpr int NARROW_R_ROWS = 64;
-bool narrow_r_ok(int P16, int64_t n_pad);  // the variant exists for this shard
-hipError_t launch_narrow_r(int P16, const PassArgs& a, int grid, hipStream_t st, hipEvent_t e0 = nullptr,
-                           hipEvent_t e1 = nullptr);
 
 // wide path (wide.hip)
 int wide_panels(int p);

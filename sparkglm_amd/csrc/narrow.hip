@@ -94,6 +94,23 @@ struct NGeo {
   static_assert(LDS * 8 <= 160 * 1024, "LDS budget");
 };
 
+// vmcnt accounting.  A wave waits for one block's DMA with s_waitcnt vmcnt(N), N = the vector-memory
+// instructions issued AFTER that DMA (vmcnt counts down in issue order).  Every wait names what it lets
+// fly -- whole block DMAs and eta stores younger than the block it needs -- and N follows from the
+// instruction counts here, which nstage / stage_next issue by construction (their loops run DMA_X
+// column-octet loads plus DMA_V row-vector load).  A loop change then changes a named operand of
+// younger(), not a literal.
+template <int P16>
+struct VmCount {
+  static constexpr int DMA_X = NGeo<P16>::NOCT;  // column-octet wave-instructions per block
+  static constexpr int DMA_V = 1;                // the y / m / offset / prior slice
+  static constexpr int DMA_BLOCK = DMA_X + DMA_V;
+  static constexpr int ETA_STORE = 1;            // one global_store_dwordx2 per block (pair)
+  static constexpr int younger(int blocks, int eta_stores) { return blocks * DMA_BLOCK + eta_stores * ETA_STORE; }
+};
+static_assert(VmCount<4>::younger(1, 1) == 4 * 16 / 8 + 2 && VmCount<1>::younger(1, 0) == 16 / 4 + 1,
+              "NOCT + 1 per block DMA (p = 64: 8 + 1; p = 16: 4 + 1), one per eta store");
+
 template <int NRB>
 __device__ __forceinline__ constexpr int swz(int c) { return NRB == 16 ? 2 * ((c >> 1) & 7) : 2 * (c & 15); }
 
@@ -126,7 +143,7 @@ __device__ __forceinline__ void nstage(double* wl, int buf, const PassArgs& a, i
   const double* xb = a.X + blk * G::NRB;
   double* dst = wl + buf * G::BUF;
 #pragma unroll
-  for (int o = 0; o < G::NOCT; ++o) {
+  for (int o = 0; o < VmCount<P16>::DMA_X; ++o) {
     const int os = o < ngrp_stored ? o : ngrp_stored - 1;  // uniform
     __builtin_amdgcn_global_load_lds((const void*)(xb + (int64_t)(G::CPI * os) * a.ld + loff[o % G::LPER]),
                                      (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * G::NRB), 16, 0, AUX);
@@ -179,6 +196,7 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false, bool T4 = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
+  using VM = VmCount<P16>;
   constexpr int NRB = G::NRB, LPR = G::LPR, CPL = G::NC / LPR;  // row stage: columns per lane
   // Poisson: per-row functions of the count y tabulated in LDS after the waves' images -- the
   // initial pass's unit deviance at mu0 and lgamma(y + 1) (rowmath.hpp poisson_init_table), the
@@ -297,7 +315,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     asm volatile("" : "+s"(cs));
     int64_t co = 0;
 #pragma unroll
-    for (int o = 0; o < G::NOCT; ++o) {
+    for (int o = 0; o < VM::DMA_X; ++o) {
       if (o > 0 && o < ngrp_stored) co += cs;  // uniform: groups past the stored columns repeat the last
       __builtin_amdgcn_global_load_lds((const void*)(dsrc[o % G::LPER] + co),
                                        (lds_void*)(dst + (o * G::CPI / 16) * G::BSTR + (o * G::CPI % 16) * NRB), 16, 0, IRLS ? DMA_NT : 0);
@@ -341,9 +359,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       double xp[KS][P16];  // the first block's Gram operands (lane (rq, cl): row 4s + rq, column 16b + cl)
       double eta_p = 0.0, y_p, m_p, off_p, pw_p;
       __builtin_amdgcn_s_setprio(PRIO_ROWS);
-      // the first block landed; the second (and the last pair's eta store) may fly
-      if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
-      else wait_vm<G::NOCT + 1>();
+      // the first block landed; younger than its DMA (issued in the last pair's first half): the
+      // last pair's eta store and the second block's DMA (the first pair: that DMA only)
+      if (has_eta && blk > b0) wait_vm<VM::younger(1, 1)>();
+      else wait_vm<VM::younger(1, 0)>();
       {
         const double* xs = wl;
         const double* vv = xs + G::XB;
@@ -360,8 +379,8 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (blk + 2 < b1) stage_next(std::integral_constant<int, 0>{});
       }
-      // the second block landed; block blk + 2 may fly
-      if (blk + 2 < b1) wait_vm<G::NOCT + 1>();
+      // the second block landed; younger than its DMA: block blk + 2's (issued above)
+      if (blk + 2 < b1) wait_vm<VM::younger(1, 0)>();
       else wait_vm<0>();
       const double* xs = wl + G::BUF;
       const double* vv = xs + G::XB;
@@ -476,10 +495,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   auto block = [&](auto bufc, int64_t blk) {
     constexpr int BUFI = decltype(bufc)::value;
     __builtin_amdgcn_s_setprio(PRIO_ROWS);
-    // block blk landed; block blk+1 (and the previous block's eta store) may still fly
+    // block blk landed; younger than its DMA: block blk + 1's and the previous block's eta store
     if (blk + 1 >= b1) wait_vm<0>();
-    else if (has_eta && blk > b0) wait_vm<G::NOCT + 2>();
-    else wait_vm<G::NOCT + 1>();
+    else if (has_eta && blk > b0) wait_vm<VM::younger(1, 1)>();
+    else wait_vm<VM::younger(1, 0)>();
     const double* xs = wl + BUFI * G::BUF;
 
     // ---- row stage ----
@@ -542,10 +561,10 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     __builtin_amdgcn_s_setprio(PRIO_ROWS);
     // the first block landed, the second may fly.  The last pair's eta store was issued before both
     // blocks' DMAs (in its row stage, ahead of the Grams), so it is older than the first block's and
-    // must not be counted as in flight: with NOCT + 2 the first block's row-vector DMA (y, offset,
+    // must not be counted as in flight: with younger(1, 1) the first block's row-vector DMA (y, offset,
     // prior) could still be landing while the row stage read it (a run-to-run difference of ~1e-6
     // in the Poisson / Gaussian passes at p > 32, tests/test_gpu_determinism.py)
-    wait_vm<G::NOCT + 1>();
+    wait_vm<VM::younger(1, 0)>();
     double eta_p = 0.0, y_p, m_p, off_p, pw_p;
     {
       const double* xs = wl;

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(L.EXPORTS) == syms
-    assert lib.sglm_abi_version() == 7
+    assert lib.sglm_abi_version() == 8
 
 
 def test_java_double_to_string():

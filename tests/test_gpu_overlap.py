@@ -116,9 +116,9 @@ def test_overlapped_lm_and_timing_split(engines):
     assert st["row_kernel_ms"] > 0 and st["gram_kernel_ms"] > 0
 
 
-def _proc_engine(chunks: int, spec: bool = True, lean: int = 1, gate: int = 2) -> Engine:
+def _proc_engine(chunks: int, spec: bool = True) -> Engine:
     env = {"SGLM_PROC_OVERLAP": str(chunks), "SGLM_PROC_OV_MIN": "4096", "SGLM_SPECULATE": "1" if spec else "0",
-           "SGLM_WIDE_OVERLAP": "1", "SGLM_PROC_LEAN": str(lean), "SGLM_PROC_OV_GATE": str(gate)}
+           "SGLM_WIDE_OVERLAP": "1"}
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -131,12 +131,15 @@ def _proc_engine(chunks: int, spec: bool = True, lean: int = 1, gate: int = 2) -
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("kind,p,fam,link", [(0, 520, "binomial", "logit"), (2, 300, "poisson", "log")])
+@pytest.mark.parametrize("kind,p,fam,link", [(0, 520, "binomial", "logit"), (2, 300, "poisson", "log"),
+                                              (2, 301, "poisson", "log"), (0, 263, "binomial", "logit")])
 def test_overlapped_procedural_chunks(kind, p, fam, link):
     """Procedural shards (X generated per pass into an HBM scratch, configs[4]'s path) with two
-    scratch buffers: the row kernel of chunk c + 1 generates while the Gram kernels of chunk c read.
-    Equal to the resident fit to rounding (another chunking), bitwise run to run and with the
-    deviance-only last pass."""
+    scratch buffers: chunk 0's generating row kernel, then for chunks >= 1 the lean generator
+    (proc_gen_kernel: X and X beta, partial sums in the resident order) and the family stage from
+    that eta, beside chunk c - 1's diagonal Gram launch.  Equal to the resident fit to rounding
+    (another chunking) at p not a multiple of 4 too (the tail columns' partial sums), bitwise run
+    to run and with the deviance-only last pass."""
     n = 30000
     ov, ov2, res = _proc_engine(6), _proc_engine(6, spec=False), _engine(1)
     try:
@@ -158,31 +161,6 @@ def test_overlapped_procedural_chunks(kind, p, fam, link):
     assert a.iter == r.iter
     d = (rel(a.coefs, r.coefs), rel(a.stderr, r.stderr), rel([a.deviance, a.pearson], [r.deviance, r.pearson]))
     assert max(d) < 1e-11, d
-
-
-@pytest.mark.parametrize("kind,p,fam,link", [(0, 520, "binomial", "logit"), (2, 301, "poisson", "log"),
-                                              (3, 263, "gamma", "inverse")])
-def test_lean_generator_is_bitwise_the_generating_row_kernel(kind, p, fam, link):
-    """SGLM_PROC_LEAN: the overlapped chunks generate X and X beta in proc_gen_kernel and run the
-    family stage from that eta (1: chunks >= 1, 2: chunk 0 too) -- bitwise the fit whose row kernel
-    generates (0), including p not a multiple of 4 (the tail columns' partial-sum order); and the
-    launch orders of SGLM_PROC_OV_GATE change nothing either."""
-    n = 24576
-    fits = []
-    for lean, gate in ((0, 2), (1, 2), (2, 2), (1, 1), (0, 0)):
-        e = _proc_engine(5, lean=lean, gate=gate)
-        try:
-            e.synth(kind, 5, n, p, 8, procedural=True)
-            assert e.stats()["overlap_chunks"] == 5
-            fits.append(e.fit_glm(fam, link))
-        finally:
-            e.close()
-    a = fits[0]
-    for f in fits[1:]:
-        np.testing.assert_array_equal(a.coefs, f.coefs)
-        np.testing.assert_array_equal(a.stderr, f.stderr)
-        assert (a.deviance, a.pearson, a.loglik, a.iter) == (f.deviance, f.pearson, f.loglik, f.iter)
-        np.testing.assert_array_equal(np.asarray(a.dev_trace), np.asarray(f.dev_trace))
 
 
 def test_overlapped_shards_of_a_multi_device_handle():

@@ -49,22 +49,13 @@ def test_kernel_choice(n, p, fs, proc, force, kind, name):
     assert L.pass_kernel_for(n, p, fused_split=fs, procedural=proc, force_wide=force) == (kind, name)
 
 
-@pytest.mark.parametrize("n,p,ns,kind,name", [
-    (125_000_000, 64, 0, "narrow", "irls_narrow_kernel<4,binomial,logit>"),      # SGLM_NARROW_SPLIT=0: never
-    (125_000_000, 64, 3, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),
-    (125_000_000, 33, 3, "narrow-split", "irls_narrow_r_kernel<3,binomial,logit>"),
-    (600_000_000, 64, 3, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),  # tall form
-    (500_000_000, 32, 2, "narrow-split", "irls_narrow_r_kernel<2,binomial,logit>"),
-    (1_000_000_000, 32, 2, "narrow-split", "irls_narrow_r_kernel<2,binomial,logit>"),  # tall form
-    (1_000_000, 16, 2, "narrow", "irls_narrow_kernel<1,binomial,logit>"),         # no one-block split variant
-    (536_870_912, 64, 4, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),  # tall form
-    (536_870_000, 64, 4, "narrow-split", "irls_narrow_r_kernel<4,binomial,logit>"),
-])
-def test_narrow_split_choice(n, p, ns, kind, name):
-    # the split-role narrow pass (narrow_r.hip) from P16 = SGLM_NARROW_SPLIT (default 0: off,
-    # slower than irls_narrow_kernel on MI355X) at any shard
-    # height (past 2^29 rows its DMA takes one column per half-wave instruction)
-    assert L.pass_kernel_for(n, p, narrow_split=ns) == (kind, name)
+@pytest.mark.parametrize("n,p", [(125_000_000, 64), (125_000_000, 33), (1_000_000_000, 32), (536_870_912, 64),
+                                 (1_000_000, 16)])
+def test_every_narrow_shard_runs_the_narrow_kernel(n, p):
+    # p <= 64 at any shard height: irls_narrow_kernel (the split-role narrow pass, measured 30-44 %
+    # slower on MI355X, was removed in round 6)
+    P16 = (p + 15) // 16
+    assert L.pass_kernel_for(n, p) == ("narrow", f"irls_narrow_kernel<{P16},binomial,logit>")
 
 
 def test_kernel_name_carries_the_family():

@@ -60,9 +60,11 @@ def test_overlap_register_budget():
 
 def test_lean_generator_fits_two_waves_beside_the_gram():
     # proc_gen_kernel (SGLM_PROC_LEAN) runs beside the off-diagonal launch: two of its waves and the
-    # two Gram waves of a SIMD must fit the 512 VGPRs together
+    # two Gram waves of a SIMD must fit the 512 VGPRs together; both design kinds (POS = true: the
+    # positive gamma design of kind 3) run there
     meta = _kernel_meta()
     off = meta["_ZN4sglm16wide_gram_kernelILb0ELb0EEEvNS_12WideGramArgsE"]
-    gen = meta["_ZN4sglm15proc_gen_kernelILb0EEEvNS_11ProcGenArgsEPKdPd"]
-    assert gen["private_segment_fixed_size"] == 0
-    assert 2 * _alloc(off["vgpr_count"]) + 2 * _alloc(gen["vgpr_count"]) <= 512, (off, gen)
+    for pos in (0, 1):
+        gen = meta[f"_ZN4sglm15proc_gen_kernelILb{pos}EEEvNS_11ProcGenArgsEPKdPd"]
+        assert gen["private_segment_fixed_size"] == 0
+        assert 2 * _alloc(off["vgpr_count"]) + 2 * _alloc(gen["vgpr_count"]) <= 512, (pos, off, gen)

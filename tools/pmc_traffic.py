@@ -28,7 +28,8 @@ WL = {  # name: (key, rows, kernel substrings of the pass, substring of the kern
 
 def load(d, wl):
     out = subprocess.run([sys.executable, os.path.join(HERE, "pmc_sum.py")] +
-                         [os.path.join(d, f"{wl}_{i}") for i in (1, 2, 3)] + ["--kernel", "sglm", "--json"],
+                         [os.path.join(d, f"{wl}_{i}") for i in (1, 2, 3, 4) if os.path.isdir(os.path.join(d, f"{wl}_{i}"))] +
+                         ["--kernel", "sglm", "--json"],
                          capture_output=True, text=True, check=True).stdout
     return json.loads(out)
 
@@ -61,12 +62,26 @@ def main():
                            "(gfx950 reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md); KB x 1024; summed "
                            "over every dispatch of the pass's kernels, per pass; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; MFMA busy = "
                            "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock cycles)"}
+        if any("SQ_INSTS_VALU_MFMA_F64" in v for v in ks.values()):
+            # group 4 (the fp64 pipe's instruction mix): wave-level instruction counts per row.  The
+            # pipe-bound time bench.py derives from them: MFMA f64 16x16x4 = 64 cycles, fp64 VALU
+            # add / mul / fma = 4 cycles (16 lanes per cycle: the 78.6 TF/s vector rate), fp64
+            # transcendental = 16 cycles, over 1024 SIMDs at the PMC clock
+            entry["fp64_mfma_insts_per_row"] = tot("SQ_INSTS_VALU_MFMA_F64") / rows
+            entry["fp64_valu_insts_per_row"] = sum(tot(c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                                     "SQ_INSTS_VALU_FMA_F64")) / rows
+            entry["fp64_trans_insts_per_row"] = tot("SQ_INSTS_VALU_TRANS_F64") / rows
+            entry["valu_insts_per_row"] = tot("SQ_INSTS_VALU") / rows
+            entry["method"] += ("; fp64 pipe mix (group 4): SQ_INSTS_VALU_MFMA_F64, SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 "
+                                "per row")
         if key in tab:
             prev = tab[key]
             entry["previous"] = {k: prev.get(k) for k in ("bytes_per_row", "clock_ghz", "mfma_busy_frac", "source")}
         tab[key] = entry
+        mix = (f"  fp64: mfma {entry['fp64_mfma_insts_per_row']:.3f} valu {entry['fp64_valu_insts_per_row']:.2f} "
+               f"trans {entry['fp64_trans_insts_per_row']:.3f} /row") if "fp64_mfma_insts_per_row" in entry else ""
         print(f"{key:20s} {entry['bytes_per_row']:9.1f} B/row (fetch {entry['fetch_bytes_per_row']:.1f}, write "
-              f"{entry['write_bytes_per_row']:.1f})  clock {entry['clock_ghz']:.2f} GHz  MFMA busy {entry['mfma_busy_frac']:.3f}")
+              f"{entry['write_bytes_per_row']:.1f})  clock {entry['clock_ghz']:.2f} GHz  MFMA busy {entry['mfma_busy_frac']:.3f}{mix}")
     json.dump(tab, open(path, "w"), indent=1)
 
 

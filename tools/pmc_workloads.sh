@@ -5,7 +5,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 run_wl() {  # name PN PP PKIND PF PL [PPROC] [VAR=value: extra environment]
   local name=$1
   export PN=$2 PP=$3 PKIND=$4 PF=$5 PL=$6 PK=2 PPROC=${7:-0}
-  env ${8:-PMC_WL=$1} bash tools/pmc_counters.sh "$name" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" || exit 1
+  # group 4: the fp64 pipe's instruction mix (MFMA + fp64 VALU), for fp64_pipe.pipe_bound_ms
+  env ${8:-PMC_WL=$1} bash tools/pmc_counters.sh "$name" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" \
+    "GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU" || exit 1
 }
 for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
   case $wl in

@@ -188,9 +188,36 @@ def mfma_clock_bound(p: int, n: int, family: str, procedural: bool = False) -> d
     clk = e.get("clock_ghz")
     t = (p + 15) // 16
     cycles = t * (t + 1) // 2 * (n / 4) * 64 / 1024
-    return {"mfma_tiles": t * (t + 1) // 2, "clock_ghz_pmc": clk, "mfma_busy_frac_pmc": e.get("mfma_busy_frac"),
-            "mfma_stream_ms_at_pmc_clock": cycles / (clk * 1e9) * 1e3 if clk else None,
-            "mfma_stream_ms_at_2p4ghz": cycles / 2.4e9 * 1e3}
+    out = {"mfma_tiles": t * (t + 1) // 2, "clock_ghz_pmc": clk, "mfma_busy_frac_pmc": e.get("mfma_busy_frac"),
+           "mfma_stream_ms_at_pmc_clock": cycles / (clk * 1e9) * 1e3 if clk else None,
+           "mfma_stream_ms_at_2p4ghz": cycles / 2.4e9 * 1e3}
+    out.update(fp64_pipe_bound(e, n))
+    return out
+
+
+# Cycles one SIMD spends per wave-instruction on the fp64 pipe (MI355X: 78.6 TF/s fp64 over 1024 SIMDs
+# at 2.4 GHz = 32 flop / cycle / SIMD): v_mfma_f64_16x16x4 (2048 flop) 64, an fp64 add / mul / fma
+# (64 lanes at 16 lanes a cycle) 4, an fp64 transcendental (quarter rate) 16.
+PIPE_CYCLES = {"mfma": 64, "valu": 4, "trans": 16}
+
+
+def fp64_pipe_bound(e: dict, n: int) -> dict:
+    """The fp64 pipe's time for a launch of n rows when the MFMA and the fp64 VALU instructions share
+    it: (MFMA cycles + fp64 VALU cycles) / 1024 SIMDs / the PMC clock, from the
+    per-row instruction mix the PMC pass measured (profiles/pmc_traffic.json, tools/pmc_workloads.sh
+    group 4: SQ_INSTS_VALU_MFMA_F64, SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64).  Empty when the stored
+    entry has no mix."""
+    clk = e.get("clock_ghz")
+    if not clk or "fp64_mfma_insts_per_row" not in e:
+        return {}
+    per_row = (e["fp64_mfma_insts_per_row"] * PIPE_CYCLES["mfma"] + e["fp64_valu_insts_per_row"] * PIPE_CYCLES["valu"]
+               + e.get("fp64_trans_insts_per_row", 0.0) * PIPE_CYCLES["trans"])
+    ms = per_row * n / 1024 / (clk * 1e9) * 1e3
+    return {"fp64_mfma_insts_per_row": e["fp64_mfma_insts_per_row"],
+            "fp64_valu_insts_per_row": e["fp64_valu_insts_per_row"],
+            "fp64_trans_insts_per_row": e.get("fp64_trans_insts_per_row", 0.0),
+            "pipe_cycles_per_row": per_row, "pipe_bound_ms": ms,
+            "pipe_bound_method": "(MFMA x 64 + fp64 VALU x 4 + fp64 transcendental x 16 cycles) / 1024 SIMDs / PMC clock"}
 
 
 def _free_port() -> int:
@@ -360,6 +387,12 @@ def main() -> int:
                     "algorithmic_bytes_per_launch": bytes_pass,
                     "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS,
                     "fp64_pipe": mfma_clock_bound(p, n, fam)}
+            # how close the pass is to the fp64 pipe's bound, and the HBM fraction that bound allows:
+            # an HBM target above it is out of reach at this clock whatever the memory system does
+            pb = roof["fp64_pipe"].get("pipe_bound_ms")
+            if pb:
+                roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
+                roof["fp64_pipe"]["hbm_frac_at_pipe_bound"] = bytes_pass / (pb * 1e-3) / 1e9 / HBM_PEAK_GBS
         else:
             roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
@@ -369,6 +402,9 @@ def main() -> int:
             # the measured kernel time: how close the kernel is to its clock-limited bound
             sm = roof["fp64_pipe"].get("mfma_stream_ms_at_pmc_clock")
             roof["fp64_pipe"]["kernel_frac_of_clock_limited_stream"] = sm / kern_ms if sm and kern_ms else None
+            pb = roof["fp64_pipe"].get("pipe_bound_ms")
+            if pb:
+                roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
         out = {
             "metric": METRIC,
             "value": total_rows * args.steps / dt,

@@ -60,9 +60,10 @@ extern "C" {
                               sglm_stats.comm_path / rank_blocks / pass_kernel_ms_min / proc_chunks /
                               proc_chunk_rows / solve_path; 6: sglm_stats.pass_kernel / pass_kernel_name,
                               sglm_set_comm_rank collective; 7: sglm_stats.lm_device_fits /
-                              lm_device_reruns; 8: sglm_create(devs, ndev) as SURVEY 8(b) names it
-                              (was sglm_create_multi), the one-device form renamed sglm_create_device,
-                              SGLM_KERNEL_NARROW_SPLIT retired */
+                              lm_device_reruns; 8: sglm_create(devs, ndev) as SURVEY 8(b) names it,
+                              the one-device form renamed sglm_create_device (sglm_create_multi stays:
+                              the group handle at any ndev), SGLM_KERNEL_NARROW_SPLIT retired,
+                              sglm_stats.lm_onepass_fits */
 
 enum sglm_status {
   SGLM_OK = 0,
@@ -200,7 +201,10 @@ typedef struct {
   int64_t lm_device_fits;   /* LM fits done in one device round trip (Gram pass, device Cholesky, residual pass;
                                resident p <= 64 shards without a communicator; SGLM_LM_DEVICE=0 disables) */
   int64_t lm_device_reruns; /* of those, fits whose device coefficients were not the host solve's bit for bit (the
-                               host left Cholesky for LU): the residual pass reran at the host's coefficients */
+                               host left Cholesky for LU) or whose one-pass statistics were flagged: the residual
+                               pass reran at the host's coefficients */
+  int64_t lm_onepass_fits;  /* of the device fits, those whose SSE / R^2 / F came from the Gram pass's sums (X'X,
+                               X'y, X'1, y'y, sum y) -- one pass over X -- instead of a residual pass */
 } sglm_stats;
 
 /* Caller-supplied all-reduce (sum, fp64, in place).  on_device != 0: buf is a device
@@ -227,6 +231,9 @@ int sglm_device_count(int *count);
 int sglm_create(const int *devs, int ndev, sglm_engine **out);
 /* One device by ordinal (the ABI <= 7 sglm_create(int, ...)). */
 int sglm_create_device(int device, sglm_engine **out);
+/* Always the multi-device (group) handle, for ndev = 1 too: a one-device group runs the RCCL
+ * group all-reduce path (ncclCommInitAll over one device) -- how tests execute it on one GPU. */
+int sglm_create_multi(const int *devs, int ndev, sglm_engine **out);
 int sglm_handle_devices(sglm_engine *h, int *ndev);
 void sglm_destroy(sglm_engine *h);
 

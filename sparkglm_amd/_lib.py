@@ -29,7 +29,7 @@ EXPORTS = [
     "sglm_irls_iterations", "sglm_predict", "sglm_get_stats", "sglm_reset_stats",
     "sglm_fit_glm_external", "sglm_fit_lm_external", "sglm_glm_create_obj", "sglm_glm_summary",
     "sglm_lm_summary", "sglm_sig_digits", "sglm_round_digits", "sglm_java_double_string",
-    "sglm_pval_normal", "sglm_pval_t", "sglm_create_device", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
+    "sglm_pval_normal", "sglm_pval_t", "sglm_create_device", "sglm_create_multi", "sglm_handle_devices", "sglm_reserve", "sglm_set_rows",
     "sglm_predict_glm", "sglm_predict_new", "sglm_local_comm_create", "sglm_local_comm_destroy",
     "sglm_local_comm_rank", "sglm_local_allreduce", "sglm_set_comm_rank", "sglm_pass_kernel_for",
 ]
@@ -64,7 +64,8 @@ class Stats(C.Structure):
                 ("overlap_chunks", C.c_int), ("comm_path", C.c_int), ("rank_blocks", C.c_int),
                 ("pass_kernel_ms_min", C.c_double), ("proc_chunks", C.c_int), ("proc_chunk_rows", C.c_int64),
                 ("solve_path", C.c_int), ("pass_kernel", C.c_int), ("pass_kernel_name", C.c_char * 64),
-                ("lm_device_fits", C.c_int64), ("lm_device_reruns", C.c_int64)]
+                ("lm_device_fits", C.c_int64), ("lm_device_reruns", C.c_int64),
+                ("lm_onepass_fits", C.c_int64)]
 
 
 COMM_PATHS = {0: "none", 1: "caller-host", 2: "caller-device", 3: "rccl", 4: "group-rccl", 5: "group-host"}
@@ -125,6 +126,7 @@ def load():
         "sglm_device_count": ([C.POINTER(C.c_int)], C.c_int),
         "sglm_create": ([C.POINTER(C.c_int), C.c_int, E], C.c_int),
         "sglm_create_device": ([C.c_int, E], C.c_int),
+        "sglm_create_multi": ([C.POINTER(C.c_int), C.c_int, E], C.c_int),
         "sglm_destroy": ([h], None),
         "sglm_set_data": ([h, dp, C.c_int64, C.c_int64, C.c_int64, dp, dp, dp, dp], C.c_int),
         "sglm_set_data_device": ([h, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,

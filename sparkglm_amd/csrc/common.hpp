@@ -64,6 +64,7 @@ struct PassArgs {
                         // pass's scalars instead of the eta store + stats_kernel
   int no_gram;          // deviance-only pass (glm_drive's speculative last pass): row stage, no Gram
   int fused_split;      // split-role kernel K1r (irls_pass_r_kernel) from P16 >= threshold: 1 default, 0 never, N: P16 >= N
+  int lm_extras;        // narrow LM Gram pass of the one-round-trip LM.fit: X'1 after the scalars, y'y in S_PEARSON
 };
 
 // ---- wide-design path (p > 16*MAX_P16): row kernel + panel-pair Gram kernel ----

@@ -244,7 +244,10 @@ int lm_drive(Backend& be, sglm_prelm* out) {
   // the device's residual statistics stand only if its solve was this one, bit for bit; a device
   // Cholesky that failed a pivot returns NaN coefficients (its statistics are never used)
   const bool dev_failed = dev && std::any_of(dev_coefs.begin(), dev_coefs.end(), [](double v) { return std::isnan(v); });
-  if (!dev || dev_failed || std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
+  // ... and only if the sums they were formed from did not cancel too far (S_BAD: lm_chol_kernel's
+  // LM_ONEPASS_MAX_RATIO guard) -- otherwise the residual pass, LM.scala:160-188's own form
+  if (!dev || dev_failed || s[S_BAD] != 0.0 ||
+      std::memcmp(dev_coefs.data(), coefs.data(), sizeof(double) * (size_t)p) != 0) {
     rc = be.stats(MODE_LM_RESID, coefs.data(), 0.0, ymean, FAM_GAUSSIAN, LNK_IDENTITY, s.data());
     if (rc) return rc;
     if (dev) be.lm_device_reruns += 1;

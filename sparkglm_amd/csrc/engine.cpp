@@ -452,7 +452,9 @@ struct sglm_engine : public Backend {
   double pass_ms = 0.0, reduce_ms = 0.0, last_pass_ms = 0.0, last_reduce_ms = 0.0, row_ms = 0.0, gram_ms = 0.0;
   int fused_split = 1;  // SGLM_FUSED_SPLIT: 1 K1r from its default column-block count up, 0 never (K1), N >= 2 from P16 = N
   bool allow_lm_device = true;  // SGLM_LM_DEVICE=0: LM fits take the two host round trips (tests)
+  bool lm_extras_pass = false;  // the next LM Gram pass also sums X'1 and y'y (lm_device, one pass)
   int64_t lm_device_fits = 0;
+  int64_t lm_onepass_fits = 0;  // of those, fits whose statistics came from the Gram pass's sums
   int last_kernel = SGLM_KERNEL_NONE;  // the kernel of the last pass (enum sglm_pass_kernel) and its name
   char last_kernel_name[64] = "";
   // ingest (sglm_reserve / sglm_set_rows): two pinned staging buffers, double-buffered
@@ -1311,6 +1313,7 @@ struct sglm_engine : public Backend {
     a.eta_out = (mode == MODE_IRLS && !a.stats_in_pass) ? deta : nullptr;
     a.no_gram = dev_only ? 1 : 0;
     a.fused_split = fused_split;
+    a.lm_extras = (mode == MODE_LM_GRAM && narrow && lm_extras_pass) ? 1 : 0;
     if (wide) {
       HIPCHK(hipEventRecord(ev0, st));
       WideRowArgs r{};
@@ -1473,7 +1476,7 @@ struct sglm_engine : public Backend {
         HIPCHK(hipEventRecord(ev1, st));
         e2 = ev2;
       }
-      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st, e2));
+      HIPCHK(launch_reduce(dpart, stride, nblocks > 0 ? grid : 1, (int)p, P16, dred, st, e2, a.lm_extras ? (int)p : 0));
       return SGLM_OK;
     }
     HIPCHK(hipEventRecord(ev2, st));
@@ -1586,47 +1589,42 @@ struct sglm_engine : public Backend {
   }
 
   // LM.fit in one round trip (driver.hpp Backend::lm_device): a resident narrow shard with no
-  // communicator -- the Gram pass, lm_chol_kernel (the host Cholesky, bitwise, on the device), the
-  // residual pass at its coefficients (beta and ybar read from the device) and the device sum of its
-  // statistics, then ONE copy back and one synchronisation.  configs[0] (1M x 20) is launch- and
-  // latency-bound: this removes the host round trip between the two passes.
+  // communicator -- the Gram pass, which also sums X'1 and y'y (narrow LMX), then lm_chol_kernel:
+  // the host Cholesky, bitwise, on the device, and the residual statistics of LM.scala:160-188 from
+  // those sums (SSE = y'y - 2 b'X'y + b'X'X b, ...; kernels.hip lm_chol_kernel), written with the
+  // whole result to pinned host memory -- ONE pass over X and one synchronisation.  Where the sums
+  // cancel too far (LM_ONEPASS_MAX_RATIO) the statistics come back flagged (S_BAD) and lm_drive runs
+  // the residual pass, the reference's own form; so does a device Cholesky that is not the host's.
+  // configs[0] (1M x 20) is launch- and latency-bound: round 5 removed the host round trip between
+  // the two passes, round 6 the second pass.
   int lm_device(double* packed, double* dev_coefs, double* s, bool& done) override {
     done = false;
     if (!allow_lm_device || group() || comm.kind != 0 || wide || procx.on || !narrow || p > 64 || nblocks <= 0)
       return SGLM_OK;
     HIPCHK(hipSetDevice(device));
-    // one device buffer, copied back in one piece: packed Gram | residual statistics [NS] | coefs [p]
+    // one device buffer, copied back in one piece: packed Gram | X'1 [p] | statistics [NS] | coefs [p]
     const int64_t plen = packed_len(p);
-    if (int rc = ensure_red_len(plen + NS + p)) return rc;
+    if (int rc = ensure_red_len(plen + p + NS + p)) return rc;
     if (int rc = ensure_small(64)) return rc;
     // a kernel that carries a completion event ends ~4.5 us later than one that does not (its
     // end-of-kernel signal; measured on the configs[0] timeline): LM fits time their Gram pass on
     // every 16th fit and count that time for the others (pass_untimed)
     const bool timed = (lm_device_fits % 16) == 0 || lm_last_pass_ms < 0.0;
-    if (int rc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, timed)) return rc;
+    lm_extras_pass = true;
+    const int prc = enqueue_pass(MODE_LM_GRAM, nullptr, 0.0, 0.0, FAM_GAUSSIAN, LNK_IDENTITY, timed);
+    lm_extras_pass = false;
+    if (prc) return prc;
     double* aux = dsmall + NS;  // {ybar, leave-Cholesky flag}
-    double* dstat = dred + plen;
-    double* dcoef = dred + plen + NS;
-    HIPCHK(launch_lm_chol(dred, (int)p, LU_SWITCH_RATIO, dcoef, aux, st));
-    StatsArgs a{};
-    a.X = dX;
-    a.ld = n_pad;
-    a.p = (int)p;
-    a.beta = dcoef;
-    a.ybar_dev = aux;
-    a.y = dy;
-    a.n = n;
-    a.family = FAM_GAUSSIAN;
-    a.link = LNK_IDENTITY;
-    a.mode = MODE_LM_RESID;
-    a.partials = dpart;
-    const int nb = stats_blocks(n);
-    HIPCHK(launch_stats(a, nb, st));
-    // the statistics sum also writes the whole result buffer into hred (pinned, device-visible): no
-    // copy blit after it
-    double* hred_dev = nullptr;
+    double* dstat = dred + plen + p;
+    double* dcoef = dred + plen + p + NS;
+    double* hred_dev = nullptr;  // the pinned result buffer as the device sees it (no copy blit)
     HIPCHK(hipHostGetDevicePointer((void**)&hred_dev, hred, 0));
-    HIPCHK(launch_reduce_stats(dpart, nb, dstat, st, dred, hred_dev, plen + NS + p));
+    LmOnePass op;
+    op.x1 = dred + plen;
+    op.stats = dstat;
+    op.host = hred_dev;
+    op.ncopy = plen + p;
+    HIPCHK(launch_lm_chol(dred, (int)p, LU_SWITCH_RATIO, dcoef, aux, st, op));
     HIPCHK(hipStreamSynchronize(st));  // (a spin on hipStreamQuery measured slower: 0.124 against 0.115 ms)
     if (timed) {
       if (int rc = pass_timing()) return rc;
@@ -1637,10 +1635,11 @@ struct sglm_engine : public Backend {
     }
     red_on_device = true;
     std::memcpy(packed, hred, sizeof(double) * plen);
-    std::memcpy(s, hred + plen, sizeof(double) * NS);
-    std::memcpy(dev_coefs, hred + plen + NS, sizeof(double) * p);
+    std::memcpy(s, hred + plen + p, sizeof(double) * NS);
+    std::memcpy(dev_coefs, hred + plen + p + NS, sizeof(double) * p);
     done = true;
     lm_device_fits += 1;
+    lm_onepass_fits += s[S_BAD] == 0.0 ? 1 : 0;
     return SGLM_OK;
   }
 
@@ -2029,15 +2028,25 @@ int sglm_create_device(int device, sglm_engine** out) {
 void sglm_destroy(sglm_engine* h) { delete h; }
 
 // SURVEY 8(b)'s constructor: one handle over devs[0..ndev).  One device: the single-device handle
-// (sglm_create_device); several: the group handle -- one shard engine per listed device, one RCCL
-// communicator per device from ncclCommInitAll when they are distinct.
+// (sglm_create_device); several: the group handle (sglm_create_multi).
 int sglm_create(const int* devs, int ndev, sglm_engine** out) {
   if (!out || !devs || ndev < 1) {
     set_error("requirement failed: devs[ndev], ndev >= 1, out handle pointer");
     return SGLM_EINVAL;
   }
   *out = nullptr;
-  if (ndev == 1) return sglm_create_device(devs[0], out);
+  return ndev == 1 ? sglm_create_device(devs[0], out) : sglm_create_multi(devs, ndev, out);
+}
+
+// The group handle: one shard engine per listed device, one RCCL communicator per device from
+// ncclCommInitAll when they are distinct -- for one device too (a one-device group runs the RCCL
+// group all-reduce path: the tests' way to execute it on a one-GPU box).
+int sglm_create_multi(const int* devs, int ndev, sglm_engine** out) {
+  if (!out || !devs || ndev < 1) {
+    set_error("requirement failed: devs[ndev], ndev >= 1, out handle pointer");
+    return SGLM_EINVAL;
+  }
+  *out = nullptr;
   auto* g = new sglm_engine();
   g->device = devs[0];
   for (int d = 0; d < ndev; ++d) {
@@ -2558,6 +2567,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
   out->pass_kernel = h->last_kernel;
   out->lm_device_fits = h->lm_device_fits;
   out->lm_device_reruns = h->lm_device_reruns;
+  out->lm_onepass_fits = h->lm_onepass_fits;
   std::memcpy(out->pass_kernel_name, h->last_kernel_name, sizeof out->pass_kernel_name);
   return SGLM_OK;
 }
@@ -2565,7 +2575,7 @@ int sglm_get_stats(sglm_engine* h, sglm_stats* out) {
 int sglm_reset_stats(sglm_engine* h) {
   if (int rc = check_handle(h)) return rc;
   for (sglm_engine* s : h->subs) (void)sglm_reset_stats(s);
-  h->passes = h->dev_passes = h->lm_device_fits = h->lm_device_reruns = 0;
+  h->passes = h->dev_passes = h->lm_device_fits = h->lm_device_reruns = h->lm_onepass_fits = 0;
   h->pass_ms = h->reduce_ms = h->last_pass_ms = h->last_reduce_ms = h->row_ms = h->gram_ms = 0.0;
   h->comm.ms = 0.0;
   h->solve_ms = 0.0;

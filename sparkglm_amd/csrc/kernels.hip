@@ -39,18 +39,19 @@ namespace sglm {
 constexpr int RED_SEG = 8, RED_EL = 256 / RED_SEG, RED_BATCH = 32;
 
 __global__ void __launch_bounds__(256) reduce_partials_kernel(const double* __restrict__ part, int64_t stride,
-                                                              int nparts, int p, int P16, double* __restrict__ out) {
-  // partial layout: T tiles of 256 | X'Wz [16*P16] | NS scalars
+                                                              int nparts, int p, int P16, double* __restrict__ out,
+                                                              int extra) {
+  // partial layout: T tiles of 256 | X'Wz [16*P16] | NS scalars | extra (the LM Gram's X'1, narrow LMX)
   __shared__ double ss[RED_SEG][RED_EL], cs[RED_SEG][RED_EL];
   const int64_t tri = (int64_t)p * (p + 1) / 2;
-  const int64_t total = tri + p + NS;
+  const int64_t total = tri + p + NS + extra;
   const int T = P16 * (P16 + 1) / 2;
   const int el = threadIdx.x % RED_EL, sg = threadIdx.x / RED_EL;
   const int g0 = (int)((int64_t)nparts * sg / RED_SEG), g1 = (int)((int64_t)nparts * (sg + 1) / RED_SEG);
   for (int64_t base = (int64_t)blockIdx.x * RED_EL; base < total; base += (int64_t)gridDim.x * RED_EL) {
     const int64_t e = base + el;
     double s = 0.0, c = 0.0;
-    const bool scal = e >= tri + p;
+    const bool scal = e >= tri + p && e < tri + p + NS;
     if (e < total) {
       int64_t src;
       if (e < tri) {
@@ -63,8 +64,10 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(const double* __re
         src = t * 256 + (i & 15) * 16 + (j & 15);
       } else if (e < tri + p) {
         src = (int64_t)T * 256 + (e - tri);
-      } else {
+      } else if (e < tri + p + NS) {
         src = (int64_t)T * 256 + 16 * P16 + (e - tri - p);
+      } else {
+        src = (int64_t)T * 256 + 16 * P16 + NS + (e - tri - p - NS);
       }
       // the segment's partials left to right, RED_BATCH loads in flight per thread (a 256-partial
       // reduce is one batch: one load latency, not four)
@@ -226,12 +229,24 @@ __global__ void __launch_bounds__(256) stats_kernel(StatsArgs a) {
 __device__ __forceinline__ double lane_bcast(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
+//
+// One pass (LmOnePass, the LM Gram pass ran with PassArgs::lm_extras): the residual statistics of
+// LM.scala:160-188 from the Gram pass's sums instead of a second pass over X --
+//   SSE = y'y - 2 b'X'y + b'X'X b,  top = b'X'X b - 2 ybar b'X'1 + n ybar^2,  bot = y'y - 2 ybar sum y + n ybar^2
+// (sum (y - Xb)^2, sum (Xb - ybar)^2, sum (y - ybar)^2 expanded).  Each is a difference of sums up to
+// max(y'y, b'X'X b, n ybar^2), so its rounding relative to the result grows with that ratio: above
+// LM_ONEPASS_MAX_RATIO (or with any of the three <= 0, e.g. an intercept-only model's top = 0) the
+// statistics are flagged (S_BAD = 1) and lm_drive reruns the residual pass, the reference's own form.
+// The fit's whole result buffer -- packed | X'1 | statistics | b -- is written to pinned host memory
+// (no copy blit, one synchronisation): the inputs copied, the statistics and b from registers.
 template <int PM>
 __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ packed, int p, double ratio_min,
-                                                     double* __restrict__ beta, double* __restrict__ aux) {
+                                                     double* __restrict__ beta, double* __restrict__ aux,
+                                                     LmOnePass op) {
 #pragma clang fp contract(off)
   constexpr int LDL = PM + 1;
   __shared__ double Ls[PM * LDL];  // L(r, c) at Ls[r LDL + c] for the back substitution
+  __shared__ double bs[PM];        // one pass: b for every lane
   const int i = threadIdx.x;
   const bool row = i < p;
   const int64_t tri = (int64_t)p * (p + 1) / 2;
@@ -281,8 +296,53 @@ __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ 
       if (i == r) tb = xr;
     }
     if (row) beta[i] = tb;
-  } else if (row) {
-    beta[i] = __builtin_nan("");  // no coefficients: the host sees NaN and runs its own residual pass
+    if (row && op.host) op.host[(beta - packed) + i] = tb;
+    if (op.stats) {  // the residual statistics from the Gram pass's sums (one pass)
+      if (i < PM) bs[i] = row ? tb : 0.0;
+      __syncthreads();
+      double ab = 0.0;  // (X'X b)_i, j ascending
+      if (row) {
+        for (int j = 0; j < p; ++j) {
+          const int64_t idx = j <= i ? (int64_t)i * (i + 1) / 2 + j : (int64_t)j * (j + 1) / 2 + i;
+          ab += packed[idx] * bs[j];
+        }
+      }
+      double q = row ? tb * ab : 0.0, bxy = row ? tb * packed[tri + i] : 0.0, bx1 = row ? tb * op.x1[i] : 0.0;
+      for (int o = 1; o < 64; o <<= 1) {  // butterfly sums: every lane holds the same totals
+        q += __shfl_xor(q, o);
+        bxy += __shfl_xor(bxy, o);
+        bx1 += __shfl_xor(bx1, o);
+      }
+      if (i == 0) {
+        const double yy = packed[tri + p + S_PEARSON], ys = packed[tri + p + S_DEV], nr = packed[tri + p + S_SUMW];
+        const double yb = ys / nr, nyb2 = nr * yb * yb;
+        const double sse = (yy - 2.0 * bxy) + q;
+        const double top = (q - 2.0 * yb * bx1) + nyb2;
+        const double bot = (yy - 2.0 * yb * ys) + nyb2;
+        const double big = fmax(yy, fmax(q, nyb2)), small = fmin(sse, fmin(top, bot));
+        const bool ok = small > 0.0 && big < LM_ONEPASS_MAX_RATIO * small && isfinite(big);
+        double sv[NS];
+        for (int k = 0; k < NS; ++k) sv[k] = 0.0;
+        sv[S_DEV] = sse;
+        sv[S_PEARSON] = top;
+        sv[S_LL] = bot;
+        sv[S_SUMW] = nr;
+        sv[S_BAD] = ok ? 0.0 : 1.0;
+        for (int k = 0; k < NS; ++k) {
+          op.stats[k] = sv[k];
+          if (op.host) op.host[(op.stats - packed) + k] = sv[k];
+        }
+      }
+    }
+  } else {
+    if (row) beta[i] = __builtin_nan("");  // no coefficients: the host sees NaN and runs its own residual pass
+    if (row && op.host) op.host[(beta - packed) + i] = __builtin_nan("");
+    if (op.stats && i == 0) {
+      for (int k = 0; k < NS; ++k) {
+        op.stats[k] = k == S_BAD ? 1.0 : 0.0;
+        if (op.host) op.host[(op.stats - packed) + k] = k == S_BAD ? 1.0 : 0.0;
+      }
+    }
   }
   double r = (row && dgi > 0.0) ? (diag * diag) / dgi : 1.0;  // chol_pivot_ratio: min over j (exact, any order)
   for (int o = 1; o < 64; o <<= 1) r = fmin(r, __shfl_xor(r, o));
@@ -290,6 +350,8 @@ __global__ void __launch_bounds__(64) lm_chol_kernel(const double* __restrict__ 
     aux[0] = packed[tri + p + S_DEV] / packed[tri + p + S_SUMW];
     aux[1] = (fail || fmin(1.0, r) < ratio_min) ? 1.0 : 0.0;
   }
+  if (op.host)  // the rest of the result buffer: the kernel's inputs packed | X'1, [0, ncopy)
+    for (int64_t k = i; k < op.ncopy; k += 64) op.host[k] = packed[k];
 }
 
 // The stats partials [nparts][NS] summed on the device into out[NS] (no D2H of the partials):
@@ -441,13 +503,14 @@ hipError_t launch_pass(int P16, const PassArgs& a, int grid, hipStream_t st, hip
   }
 }
 
-hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st) {
+hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st,
+                          const LmOnePass& op) {
   if (p < 1 || p > 64) return hipErrorInvalidValue;
   // PM = p rounded up to 4 up to 32, to 8 above (identity padding: a padding step costs what a real one does)
   const int pm = p <= 32 ? (p + 3) / 4 * 4 : (p + 7) / 8 * 8;
   switch (pm) {
 #define SGLM_CHOL_CASE(PM) \
-  case PM: hipLaunchKernelGGL(lm_chol_kernel<PM>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux); break;
+  case PM: hipLaunchKernelGGL(lm_chol_kernel<PM>, dim3(1), dim3(64), 0, st, packed, p, ratio_min, beta, aux, op); break;
     SGLM_CHOL_CASE(4) SGLM_CHOL_CASE(8) SGLM_CHOL_CASE(12) SGLM_CHOL_CASE(16) SGLM_CHOL_CASE(20) SGLM_CHOL_CASE(24)
     SGLM_CHOL_CASE(28) SGLM_CHOL_CASE(32) SGLM_CHOL_CASE(40) SGLM_CHOL_CASE(48) SGLM_CHOL_CASE(56) SGLM_CHOL_CASE(64)
 #undef SGLM_CHOL_CASE
@@ -495,12 +558,12 @@ hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st,
-                         hipEvent_t e1) {
-  const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS;
+                         hipEvent_t e1, int extra) {
+  const int64_t total = (int64_t)p * (p + 1) / 2 + p + NS + extra;
   int blocks = (int)((total + RED_EL - 1) / RED_EL);
   if (blocks > 8192) blocks = 8192;
   hipExtLaunchKernelGGL(reduce_partials_kernel, dim3(blocks), dim3(256), 0, st, nullptr, e1, 0, part, stride, nparts, p, P16,
-                        out);
+                        out, extra);
   return hipGetLastError();
 }
 

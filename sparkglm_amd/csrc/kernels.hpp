@@ -23,10 +23,23 @@ hipError_t launch_stats(const StatsArgs& a, int grid, hipStream_t st);
 // [nparts][NS] -> [NS]; host != null: also src[0, ncopy) (out inside it) into host memory the device can write
 hipError_t launch_reduce_stats(const double* part, int nparts, double* out, hipStream_t st, const double* src = nullptr,
                                double* host = nullptr, int64_t ncopy = 0);
-// LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}
-hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st);
+// LM.fit's solve on the device, bitwise the host Cholesky (p <= 64): beta[p], aux = {ybar, leave-Cholesky flag}.
+// One pass (op.stats set; the Gram pass ran with PassArgs::lm_extras): also the residual statistics from
+// the Gram pass's sums (x1 = X'1 [p] right after the packed Gram) into op.stats; with op.host the
+// result buffer -- packed[0, ncopy) and beta / op.stats (which lie inside the same allocation past it,
+// at the same offsets) -- is written to pinned host memory.
+struct LmOnePass {
+  const double* x1 = nullptr;
+  double* stats = nullptr;  // [NS]: SSE, top, bot, rows, S_BAD = 1 when lm_drive must rerun the residual pass
+  double* host = nullptr;
+  int64_t ncopy = 0;
+};
+constexpr double LM_ONEPASS_MAX_RATIO = 1e4;  // max(y'y, b'X'Xb, n ybar^2) / min(SSE, top, bot) at most
+hipError_t launch_lm_chol(const double* packed, int p, double ratio_min, double* beta, double* aux, hipStream_t st,
+                          const LmOnePass& op = LmOnePass{});
+// extra: elements past the NS scalars summed too (the LM Gram's X'1, narrow LMX), out[tri + p + NS + k]
 hipError_t launch_reduce(const double* part, int64_t stride, int nparts, int p, int P16, double* out, hipStream_t st,
-                         hipEvent_t e1 = nullptr);
+                         hipEvent_t e1 = nullptr, int extra = 0);
 hipError_t launch_predict(const double* X, int64_t ld, int p, int64_t n, const double* beta, const double* off,
                           double* out, hipStream_t st, const ProcX& g);
 hipError_t launch_unlink(double* v, const double* m, int64_t n, int family, int link, hipStream_t st);

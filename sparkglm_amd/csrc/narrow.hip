@@ -87,10 +87,12 @@ struct NGeo {
   // MFMAs run from registers.  Half the family-arithmetic instructions per row.
   static constexpr bool PAIR = NRB == 32;
   static constexpr int WAVE_LDS = OFF_W + 4 * NRB;  // doubles per wave (w / w*z of a block pair)
-  static constexpr int PSZ = T * 256 + NC + 5;       // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad)
+  // one wave partial (tiles | X'Wz | dev, sum w, pearson, ll, bad | LMX: X'1)
+  static constexpr int PSZ = T * 256 + NC + 5 + NC;
   static constexpr int LDS = (NW * WAVE_LDS > (NW / 2) * PSZ) ? NW * WAVE_LDS : (NW / 2) * PSZ;
   static_assert(NW % 4 == 0, "whole waves per SIMD");
-  static constexpr int STRIDE = T * 256 + NC + NS;   // global partial (reduce_partials_kernel layout)
+  // global partial (reduce_partials_kernel layout): tiles | X'Wz | NS scalars | LMX: X'1 [NC]
+  static constexpr int STRIDE = T * 256 + NC + NS + NC;
   static_assert(LDS * 8 <= 160 * 1024, "LDS budget");
 };
 
@@ -193,7 +195,10 @@ __device__ __forceinline__ void gram_kstep(d4 (&acc)[NGeo<P16>::T], const double
 // carries them (no stats_kernel pass; the eta store was ~6 % of a p = 32 pass, ~1 % at p = 64).
 // The Poisson / Gamma statistics' per-fit constants (rowmath.hpp init_stats_const) are summed by
 // the initial pass (IRLS = false) into S_AUX2.
-template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false, bool T4 = false>
+// LMX (the LM Gram pass of LM.fit's one device round trip, PassArgs::lm_extras): the pass also sums
+// X'1 (column sums) and y'y, from which lm_chol_kernel forms the residual statistics without a second
+// pass over X (SSE = y'y - 2 b'X'y + b'X'X b, LM.scala:160-188's three sums; engine.cpp lm_device).
+template <int P16, int FAM, int LNK, bool IRLS, bool STATS = false, bool T4 = false, bool LMX = false>
 __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(PassArgs a) {
   using G = NGeo<P16>;
   using VM = VmCount<P16>;
@@ -233,7 +238,8 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   const bool has_eta = irls && !STATS && a.eta_out != nullptr;
   // the initial pass of a Poisson / Gamma fit sums the in-pass statistics' constants (S_AUX2)
   constexpr bool INIT_CONST = !IRLS && (FAM == FAM_POISSON || FAM == FAM_GAMMA);
-  constexpr bool XS = STATS || INIT_CONST;  // the extra scalar accumulators are live
+  static_assert(!LMX || (!IRLS && !STATS && FAM == FAM_GAUSSIAN), "LMX: the LM Gram pass");
+  constexpr bool XS = STATS || INIT_CONST || LMX;  // the extra scalar accumulators are live
   using SL = StatsSlots<FAM>;
 
   // per-lane parts of the DMA source addresses: lane -> (column cc of the group, row pair j);
@@ -265,9 +271,12 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   d4 acc[G::T];
 #pragma unroll
   for (int t = 0; t < G::T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-  double xz[P16];
+  double xz[P16], x1[P16];
 #pragma unroll
   for (int b = 0; b < P16; ++b) xz[b] = 0.0;
+  if constexpr (LMX)
+#pragma unroll
+    for (int b = 0; b < P16; ++b) x1[b] = 0.0;
   double s_dev = 0.0, s_aux = 0.0, s_pear = 0.0, s_ll = 0.0, s_bad = 0.0;
 
   const int cl = lane & 15, rq = lane >> 4;
@@ -404,6 +413,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
             pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                      !IRLS, ylogy);
+            if constexpr (LMX) s_pear += y * y;
             if constexpr (INIT_CONST)
               if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
           }
@@ -435,6 +445,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
               xk[b] = h == 0 ? xp[k][b] : xc[k][b];
               av[b] = xk[b] * wr;
               xz[b] += xk[b] * wzr;
+              if constexpr (LMX) x1[b] += xk[b];
             }
             gram_kstep<P16, T4>(acc, av, xk);
           }
@@ -463,6 +474,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           else if (!(PTAB && poisson_init_row(pconst, ptab, yv, ov, pv, w, wz, s_dev, s_aux, s_ll))) {
             pass_row(FAM, LNK, mode, eta, yv, mv, ov, pv, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                      !IRLS, ylogy);
+            if constexpr (LMX) s_pear += yv * yv;
             if constexpr (INIT_CONST)
               if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(yv, pv);
           }
@@ -482,6 +494,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
             xk[b] = xs[goff[k] + G::BSTR * b];
             av[b] = xk[b] * wr;
             xz[b] += xk[b] * wzr;
+            if constexpr (LMX) x1[b] += xk[b];
           }
           gram_kstep<P16, T4>(acc, av, xk);
         }
@@ -521,6 +534,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
           pass_row(FAM, LNK, mode, eta, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                    !IRLS, ylogy);
+          if constexpr (LMX) s_pear += y * y;
           if constexpr (INIT_CONST)
             if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
         }
@@ -542,6 +556,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           xv[b] = xs[goff[s] + G::BSTR * b];
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
+          if constexpr (LMX) x1[b] += xv[b];
         }
         gram_kstep<P16, T4>(acc, av, xv);
       }
@@ -600,6 +615,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         else if (!(PTAB && poisson_init_row(pconst, ptab, y, off, pw, w, wz, s_dev, s_aux, s_ll))) {
           pass_row(FAM, LNK, mode, et, y, m, off, pw, a.mu0, a.ybar, a.m != nullptr, w, wz, s_dev, s_aux, true,
                    !IRLS, ylogy);
+          if constexpr (LMX) s_pear += y * y;
           if constexpr (INIT_CONST)
             if (mode != MODE_LM_GRAM) s_ll += init_stats_const<FAM>(y, pw);
         }
@@ -621,6 +637,7 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
           xv[b] = xs[goff[s2] + G::BSTR * b];
           av[b] = xv[b] * wr;
           xz[b] += xv[b] * wzr;
+          if constexpr (LMX) x1[b] += xv[b];
         }
         gram_kstep<P16, T4>(acc, av, xv);
       }
@@ -645,6 +662,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
   // ---- wave partial: X'Wz over the 4 row lanes of each column, scalars over the wave ----
 #pragma unroll
   for (int b = 0; b < P16; ++b) xz[b] = xor32_sum(xor16_sum(xz[b]));
+  if constexpr (LMX)
+#pragma unroll
+    for (int b = 0; b < P16; ++b) x1[b] = xor32_sum(xor16_sum(x1[b]));
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     s_dev += __shfl_xor(s_dev, o);
@@ -672,6 +692,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       if (lane < 16) {
 #pragma unroll
         for (int b = 0; b < P16; ++b) reg[G::T * 256 + 16 * b + lane] = xz[b];
+        if constexpr (LMX)
+#pragma unroll
+          for (int b = 0; b < P16; ++b) reg[G::T * 256 + G::NC + 5 + 16 * b + lane] = x1[b];
       }
       if (lane == 0) {
         reg[G::T * 256 + G::NC] = s_dev;
@@ -690,6 +713,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
         for (int j = 0; j < 4; ++j) acc[t][j] += reg[t * 256 + 64 * j + lane];
 #pragma unroll
       for (int b = 0; b < P16; ++b) xz[b] += reg[G::T * 256 + 16 * b + (lane & 15)];
+      if constexpr (LMX)
+#pragma unroll
+        for (int b = 0; b < P16; ++b) x1[b] += reg[G::T * 256 + G::NC + 5 + 16 * b + (lane & 15)];
       s_dev += reg[G::T * 256 + G::NC];
       s_aux += reg[G::T * 256 + G::NC + 1];
       if constexpr (XS) {
@@ -714,6 +740,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
     if (lane < 16) {
 #pragma unroll
       for (int b = 0; b < P16; ++b) out[G::T * 256 + 16 * b + lane] = xz[b];
+      if constexpr (LMX)
+#pragma unroll
+        for (int b = 0; b < P16; ++b) out[G::T * 256 + G::NC + NS + 16 * b + lane] = x1[b];
     }
     if (lane < NS) {
       double v = lane == S_DEV ? s_dev : lane == S_SUMW ? s_aux : 0.0;
@@ -725,6 +754,9 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
       if constexpr (INIT_CONST) {
         if (lane == S_AUX2) v = s_ll;
       }
+      if constexpr (LMX) {
+        if (lane == S_PEARSON) v = s_pear;  // y'y
+      }
       out[G::T * 256 + G::NC + lane] = v;
     }
   }
@@ -733,6 +765,17 @@ __global__ void __launch_bounds__(64 * NGeo<P16>::NW, 1) irls_narrow_kernel(Pass
 template <int P16, int FAM, int LNK>
 void launch_narrow_fl(const PassArgs& a, dim3 gr, dim3 bl, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   constexpr bool SP = stats_in_pass_family(FAM, LNK);
+  if constexpr (FAM == FAM_GAUSSIAN) {  // the LM Gram of the one-round-trip LM.fit: X'1 and y'y too
+    if (a.mode == MODE_LM_GRAM && a.lm_extras) {
+      if (P16 == 2 && a.p <= 20)
+        hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false, false, P16 == 2, true>), gr, bl, 0, st, e0, e1,
+                              0, a);
+      else
+        hipExtLaunchKernelGGL((irls_narrow_kernel<P16, FAM, LNK, false, false, false, true>), gr, bl, 0, st, e0, e1, 0,
+                              a);
+      return;
+    }
+  }
   if constexpr (P16 == 2 && FAM == FAM_GAUSSIAN) {  // LM Gram / gaussian at p <= 20 (gram_kstep T4)
     if (a.p <= 20) {
       if (a.mode == MODE_IRLS)
@@ -775,7 +818,7 @@ hipError_t launch_narrow_p(const PassArgs& a, int grid, hipStream_t st, hipEvent
 }  // namespace
 
 int narrow_variant(int p) { return (p + 15) / 16; }
-int narrow_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS; }
+int narrow_stride(int P16) { return (P16 * (P16 + 1) / 2) * 256 + 16 * P16 + NS + 16 * P16; }  // NGeo::STRIDE
 int narrow_wg_per_cu() { return 1; }
 int narrow_rows_per_wg(int P16) {
   switch (P16) {

@@ -248,9 +248,10 @@ __device__ __forceinline__ void pass_row_init(const double* c, double y, double 
 // partition loop body GLM.scala:282-301): w and w*z for the Gramian, and the deviance.
 // LM gram mode: w = 1, z = y, and the sums of y and of rows (LM.scala:142-155, 167).
 // small_exp and init_fast are compile-time constants at every call site.
-// small_exp selects exp_small over libm's exp:
-// measured faster in the p <= 32 narrow pass (-1 %), slower at p = 64 (+4 %) and neutral in
-// the fused / wide kernels, so only the p <= 32 narrow variants set it.
+// small_exp selects exp_small over libm's exp.  Every narrow variant (p <= 64) passes true: round 4
+// measured it -1 % at p <= 32 and +4 % at p = 64 on that round's narrow kernel; round 5's rework of
+// the narrow pass (row stage at raised issue priority, block pairs at p > 32) set it for every width
+// without a separate p = 64 A/B of this choice.  The fused / wide kernels leave it off (neutral).
 // ylogy (the narrow kernel's Poisson IRLS passes): an LDS table of k log k for the integer counts
 // k < POIS_TAB (poisson_ylogy_table), so that those rows need no log: the Poisson unit deviance
 // y log(y / mu) - (y - mu) = (y log y - y eta) - (y - mu) with y log y looked up.  The deviance stays

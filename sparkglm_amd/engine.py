@@ -62,19 +62,22 @@ def glm_opts(family="binomial", link="logit", tol=1e-6, verbose=False, max_iter=
 
 
 class Engine:
-    """One HIP device holding one row shard of the design in HBM -- or, with `devices=[...]`,
-    one handle over several devices (sglm_create(devs, ndev): row shards per device, one RCCL
-    group all-reduce per iteration; a device listed twice shares the card and sums on the host).
-    Both go through SURVEY 8(b)'s constructor sglm_create(const int* devs, int ndev, ...)."""
+    """One HIP device holding one row shard of the design in HBM (SURVEY 8(b)'s constructor
+    sglm_create(const int* devs, int ndev = 1)) -- or, with `devices=[...]`, the group handle over
+    those devices (sglm_create_multi: row shards per device, one RCCL group all-reduce per
+    iteration, for one listed device too; a device listed twice shares the card and sums on the
+    host)."""
 
     def __init__(self, device: int = 0, devices=None):
         self._lib = L.load()
         h = C.c_void_p()
         if devices is not None:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            L.check(self._lib.sglm_create_multi(devs, len(devices), C.byref(h)), "sglm_create_multi")
             device = int(devices[0])
-        devs_l = [int(d) for d in devices] if devices is not None else [int(device)]
-        devs = (C.c_int * len(devs_l))(*devs_l)
-        L.check(self._lib.sglm_create(devs, len(devs_l), C.byref(h)), "sglm_create")
+        else:
+            one = (C.c_int * 1)(int(device))
+            L.check(self._lib.sglm_create(one, 1, C.byref(h)), "sglm_create")
         self._h = h
         self.device = device
         self.devices = list(devices) if devices is not None else [device]

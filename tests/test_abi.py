@@ -123,3 +123,35 @@ def test_create_without_gpu_fails_loudly():
     from sparkglm_amd import Engine
     with pytest.raises(L.SGLMError):
         Engine(0)
+
+
+def test_create_takes_a_device_list_and_refuses_bad_arguments():
+    """SURVEY 8(b)'s constructor sglm_create(const int* devs, int ndev, ...): the requires fail with
+    SGLM_EINVAL before any device is touched; on a host without a GPU a valid list fails with
+    SGLM_EHIP (loudly, no CPU fallback)."""
+    lib = L.load()
+    h = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert lib.sglm_create(None, 1, C.byref(h)) == 1 and not h.value
+    assert lib.sglm_create(devs, 0, C.byref(h)) == 1
+    assert lib.sglm_create(devs, 1, None) == 1
+    assert lib.sglm_create_multi(devs, 0, C.byref(h)) == 1
+    import torch
+    if not torch.cuda.is_available():
+        assert lib.sglm_create(devs, 1, C.byref(h)) == 3 and not h.value
+        assert lib.sglm_create_device(0, C.byref(h)) == 3
+
+
+def test_integration_knob_table_equals_the_getenv_list():
+    """Every environment knob the engine reads (getenv in csrc/) is documented in INTEGRATION.md's
+    runtime-knob table, and the table lists no knob the engine no longer reads."""
+    src = ""
+    for f in os.listdir(os.path.join(ROOT, "sparkglm_amd", "csrc")):
+        if f.endswith((".cpp", ".hpp", ".hip")):
+            src += open(os.path.join(ROOT, "sparkglm_amd", "csrc", f)).read()
+    read = set(re.findall(r'getenv\("(SGLM_[A-Z0-9_]+)"\)', src))
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    table = doc[doc.index("## Runtime knobs"):]
+    rows = set(re.findall(r"^\| `(SGLM_[A-Z0-9_]+)`(?:, `(SGLM_[A-Z0-9_]+)`)?", table, flags=re.M))
+    listed = {k for r in rows for k in r if k} - {"SGLM_LIB"}  # SGLM_LIB: the Python mirror's, not the engine's
+    assert read == listed, (read - listed, listed - read)

@@ -202,3 +202,19 @@ def test_pmc_traffic_counts_every_dispatch_of_a_pass(tmp_path, monkeypatch):
     assert abs(e["fetch_bytes_per_row"] - per_pass_kb * 2 * 1024 / rows) < 1e-9
     assert abs(e["write_bytes_per_row"] - 1.0 * 6 / 2 * 1024 / rows) < 1e-9
     assert abs(e["kernel_ms_profiled"] - (1.0 + 30.0)) < 1e-12
+
+
+def test_fp64_pipe_bound_reproduces_from_the_stored_pmc_mix():
+    # an HBM-bound line carries the fp64 pipe's bound -- (MFMA x 64 + fp64 VALU x 4
+    # + transcendental x 16 cycles) / 1024 SIMDs / PMC clock -- from profiles/pmc_traffic.json's
+    # instruction mix, so kernel_frac_of_pipe_bound reproduces from profiles/
+    e = bench.pmc_entry(64, "poisson")
+    assert e["fp64_mfma_insts_per_row"] == 2.5  # 10 lower-triangular 16x16 tiles per 4 rows: the counter's scale
+    b = bench.mfma_clock_bound(64, 125_000_000, "poisson")
+    cyc = 2.5 * 64 + e["fp64_valu_insts_per_row"] * 4 + e["fp64_trans_insts_per_row"] * 16
+    assert abs(b["pipe_cycles_per_row"] - cyc) < 1e-9
+    assert abs(b["pipe_bound_ms"] - cyc * 125_000_000 / 1024 / (e["clock_ghz"] * 1e9) * 1e3) < 1e-9
+    # at p = 64 the pipe bound sits below the 70 % HBM target: 536 B / row at the bound < 0.7 x 8 TB/s
+    hbm_frac = 125_000_000 * 536 / (b["pipe_bound_ms"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS
+    assert 0.55 < hbm_frac < 0.70
+    assert bench.fp64_pipe_bound({"clock_ghz": 2.0}, 10) == {}  # no stored mix: no bound claimed

@@ -1,11 +1,14 @@
-"""LM.fit in one device round trip (engine.cpp lm_device; driver.cpp lm_drive): the LM Gram pass,
-the host Cholesky restated on the device (lm_chol_kernel, the same operation order, no contraction),
-the residual pass at those coefficients with beta and ybar read from the device, and the device sum
-of its statistics -- one copy back and one synchronisation per fit (BASELINE configs[0] is launch-
-and latency-bound).  lm_drive keeps its host solve as the arbiter: the device path must give BITWISE
-the fit of the two-round-trip path (SGLM_LM_DEVICE=0), and where the host leaves Cholesky for the
-reference's LU inverse (an ill-conditioned X'X) the residual pass is rerun at the host's
-coefficients -- bitwise the host path again (LM.scala:142-237, 241-274)."""
+"""LM.fit in one device round trip and one pass over X (engine.cpp lm_device; driver.cpp lm_drive):
+the LM Gram pass also sums X'1 and y'y (narrow LMX), lm_chol_kernel restates the host Cholesky on the
+device (the same operation order, no contraction) and forms LM.scala:160-188's three residual sums
+from the Gram pass's sums -- SSE = y'y - 2 b'X'y + b'X'X b, sum (Xb - ybar)^2, sum (y - ybar)^2 --
+then one copy back and one synchronisation per fit (BASELINE configs[0] is launch- and latency-
+bound).  lm_drive keeps its host solve as the arbiter: the coefficients and inv(X'X) are BITWISE those
+of the two-round-trip path (SGLM_LM_DEVICE=0, which runs the reference's residual pass); the
+statistics agree with it to rounding (1e-12 here; the oracle bar is 1e-9).  Where the sums cancel
+(LM_ONEPASS_MAX_RATIO, e.g. an intercept-only model, whose sum (Xb - ybar)^2 is 0), or the host
+leaves Cholesky for the reference's LU inverse (an ill-conditioned X'X), lm_drive reruns the residual
+pass at the host's coefficients -- bitwise the host path again (LM.scala:142-237, 241-274)."""
 import os
 
 import numpy as np
@@ -37,23 +40,31 @@ def _fits(load):
             load(e)
             f = e.fit_lm()
             st = e.stats()
-            out[device] = (f, st["lm_device_fits"], st["lm_device_reruns"])
+            out[device] = (f, st["lm_device_fits"], st["lm_device_reruns"], st["lm_onepass_fits"])
     return out
 
 
-def _same(a, b):
-    for k in ("coefs", "stderr", "xtxi"):
+def _same(a, b, onepass=False, tol=1e-12):
+    """The device fit against the host path's: coefficients and inv(X'X) bitwise; the statistics
+    bitwise when the device reran the residual pass, to rounding (`tol`) when they came from the sums."""
+    for k in ("coefs", "xtxi"):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
-    # (array_equal: an intercept-only model's F statistic is NaN on both paths)
-    np.testing.assert_array_equal([a.sse, a.r2, a.fstat, a.sigma, a.nrow], [b.sse, b.r2, b.fstat, b.sigma, b.nrow])
+    sa, sb = [a.sse, a.r2, a.fstat, a.sigma, a.nrow], [b.sse, b.r2, b.fstat, b.sigma, b.nrow]
+    if onepass:
+        assert rel(sa, sb) < tol and rel(a.stderr, b.stderr) < tol, (rel(sa, sb), rel(a.stderr, b.stderr))
+    else:
+        # (array_equal: an intercept-only model's F statistic is NaN on both paths)
+        np.testing.assert_array_equal(sa, sb)
+        np.testing.assert_array_equal(a.stderr, b.stderr)
 
 
 def test_config0_design_bitwise_the_host_path_and_the_oracle():
     n, p = 1_000_000, 20
     res = _fits(lambda e: e.synth(1, 0, n, p, 1))
-    (fd, nd, rd), (fh, nh, _) = res[True], res[False]
+    (fd, nd, rd, od), (fh, nh, _, _) = res[True], res[False]
     assert nd == 1 and nh == 0 and rd == 0  # the device Cholesky's coefficients were the host's, bitwise
-    _same(fd, fh)
+    assert od == 1  # one pass over X: the statistics from the Gram pass's sums
+    _same(fd, fh, onepass=True)
     X, y, _, _ = synth.generate(1, 0, n, p, 1)
     r = po.fit_lm(X, y, nthreads=8)
     assert rel(fd.coefs, r["coefs"]) < 1e-9 and rel(fd.stderr, r["stderr"]) < 1e-9
@@ -67,8 +78,13 @@ def test_widths_bitwise_the_host_path(p):
     X = np.column_stack([np.ones(n), rng.uniform(-1, 1, (n, p - 1))]) if p > 1 else np.ones((n, 1))
     y = X @ rng.normal(size=p) + rng.uniform(-1, 1, n)
     res = _fits(lambda e: e.set_data(X, y))
-    assert res[True][1] == 1 and res[True][2] == 0  # device coefficients bitwise the host solve's
-    _same(res[True][0], res[False][0])
+    _, nd, rd, od = res[True]
+    assert nd == 1
+    if p == 1:  # intercept only: sum (Xb - ybar)^2 cancels to rounding -> flagged, the residual pass
+        assert od == 0 and rd == 1
+    else:  # device coefficients bitwise the host solve's, the statistics from the sums
+        assert od == 1 and rd == 0
+    _same(res[True][0], res[False][0], onepass=od == 1)
 
 
 def test_ill_conditioned_falls_back_to_the_host_lu():
@@ -81,7 +97,7 @@ def test_ill_conditioned_falls_back_to_the_host_lu():
     y = X @ np.array([1.0, 2.0, -1.0, 0.5, 0.25, -0.75]) + rng.uniform(-1, 1, n)
     res = _fits(lambda e: e.set_data(X, y))
     assert res[True][1] == 1 and res[True][2] == 1  # flagged on the device, rerun at the LU coefficients
-    _same(res[True][0], res[False][0])
+    _same(res[True][0], res[False][0])  # the residual pass at the host's coefficients: bitwise
     r = po.fit_lm(X, y)
     assert rel(res[True][0].sse, r["sse"]) < 1e-9
 
@@ -139,3 +155,27 @@ def test_last_column_block_on_4x4_mfma_matches_the_oracle(p):
     assert g.iter == o.iter
     assert rel(g.coefs, o.coefs) < 1e-9 and rel(g.stderr, o.stderr) < 1e-9
     assert rel([g.deviance, g.null_deviance], [o.deviance, o.null_deviance]) < 1e-9
+
+
+@pytest.mark.parametrize("shift", [0.0, 30.0, 1e2, 1e4])
+def test_onepass_statistics_guard_against_cancellation(shift):
+    """y shifted far from 0 (y'y >> SSE, bot): past LM_ONEPASS_MAX_RATIO = 1e4 of max(y'y, b'X'Xb,
+    n ybar^2) over min(SSE, top, bot) the sums cancel too far and the statistics come from the residual
+    pass (bitwise the host path); below it from the sums, within 1e-12 of the host path.  The oracle
+    bar (1e-9) holds either way."""
+    rng = np.random.default_rng(21)
+    n, p = 100_003, 6
+    X = np.column_stack([np.ones(n), rng.uniform(-1, 1, (n, p - 1))])
+    y = shift + X @ rng.normal(size=p) + rng.uniform(-1, 1, n)
+    res = _fits(lambda e: e.set_data(X, y))
+    fd, nd, rd, od = res[True]
+    r = po.fit_lm(X, y)
+    fit = X @ r["coefs"]
+    yb = y.mean()
+    big = max(float(y @ y), float(fit @ fit), n * yb * yb)
+    small = min(r["sse"], float(np.sum((fit - yb) ** 2)), float(np.sum((y - yb) ** 2)))
+    assert abs(np.log10(big / small) - 4.0) > 0.2  # (no case sits on the guard's edge)
+    assert od == (1 if big < 1e4 * small else 0), big / small
+    # the sums' rounding relative to the statistics grows with big / small (5.5e3 at shift 30)
+    _same(fd, res[False][0], onepass=od == 1, tol=max(1e-12, 1e-14 * big / small))
+    assert rel([fd.sse, fd.r2, fd.fstat, fd.sigma], [r["sse"], r["r2"], r["fstat"], r["sigma"]]) < 1e-9

@@ -1,23 +1,15 @@
 #!/bin/bash
-# Round-5 GPU session: stages as in r04_gpu.sh (test, bench, benchw, ab, ...).
+# GPU session stages (one gpurun call runs the listed ones in order; each GPU step under its own timeout):
+#   test      pytest -m gpu + smoke()            bench    the default bench line (configs[1] + 1B x 32)
+#   benchw    WORKLOADS="..." bench lines         lm       configs[0] LM timeline + rocprof
+#   sweep     mid-width sweep (+ rocprof)        cap      full-size configs[3] Gram capture
+#   rehearse8 8 ranks over gloo on one GPU        pmcab    PMC of one workload under PMCAB_LIBS
+#   abbit     bitwise pass hash + time over ABBIT_LIBS
+# usage: bash tools/gpu_stages.sh test,bench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 STAGES=${1:-cap,test,bench}
-if [[ ,$STAGES, == *,ab64,* ]]; then  # narrow p = 64 / 48 / 32: the A/B library (abl/base) against the tree
-  export AB_LIBS=${AB64_LIBS:-abl/base/libsglm_hip.so@SGLM_NARROW_SPLIT=0,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=${AB_REPS:-2}
-  for spec in ${AB64_CASES:-125000000:64:2:poisson:log 150000000:48:0:binomial:logit}; do
-    IFS=: read AN AP AK AF AL <<< "$spec"
-    AN=$AN AP=$AP AK=$AK AF=$AF AL=$AL timeout -k 10 300 python tools/ab.py >> gpurun_out/ab64.log 2>&1 || { echo "ab64 failed"; tail gpurun_out/ab64.log; exit 1; }
-  done
-  cat gpurun_out/ab64.log
-fi
-if [[ ,$STAGES, == *,nr,* ]]; then  # split-role narrow pass: parity against irls_narrow_kernel, then pass times
-  timeout -k 10 300 python -u tools/nr_check.py parity > gpurun_out/nr_parity.log 2>&1 || { echo "nr parity failed"; tail -30 gpurun_out/nr_parity.log; exit 1; }
-  cat gpurun_out/nr_parity.log
-  timeout -k 10 300 python -u tools/nr_check.py timing > gpurun_out/nr_timing.log 2>&1 || { echo "nr timing failed"; tail -30 gpurun_out/nr_timing.log; exit 1; }
-  cat gpurun_out/nr_timing.log
-fi
 if [[ ,$STAGES, == *,cap,* ]]; then
   timeout -k 10 300 python -u tools/gram_split_capture.py > gpurun_out/cap.log 2>&1 || { echo "capture failed"; tail -20 gpurun_out/cap.log; exit 1; }
   tail -3 gpurun_out/cap.log
@@ -27,19 +19,6 @@ if [[ ,$STAGES, == *,test,* ]]; then
   tail -3 gpurun_out/pytest_gpu.log
   timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
   cat gpurun_out/smoke.log
-fi
-if [[ ,$STAGES, == *,ab,* ]]; then  # same-box A/B: the round-3 library (lib_ab/head) against the tree
-  export AB_LIBS=sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so AB_REPS=3
-  AN=200000000 AP=32 AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p32.log 2>&1 || { echo "ab p32 failed"; tail gpurun_out/ab_p32.log; exit 1; }
-  AN=125000000 AP=64 AK=2 AF=poisson AL=log timeout -k 10 300 python tools/ab.py > gpurun_out/ab_p64.log 2>&1 || { echo "ab p64 failed"; tail gpurun_out/ab_p64.log; exit 1; }
-  cat gpurun_out/ab_p32.log gpurun_out/ab_p64.log
-fi
-if [[ ,$STAGES, == *,abmid,* ]]; then  # mid-width fused pass: AB_LIBS (default head, tree) at p = 80 / 96 / 112 / 128 / 240
-  export AB_LIBS=${AB_MID_LIBS:-sparkglm_amd/lib_ab/head/libsglm_hip.so,sparkglm_amd/lib/libsglm_hip.so} AB_REPS=2
-  for pn in ${AB_MID_P:-80:37500000 96:31250000 112:26785714 128:23437500 240:10000000}; do
-    AN=${pn#*:} AP=${pn%:*} AK=0 AF=binomial AL=logit timeout -k 10 300 python tools/ab.py >> gpurun_out/ab_mid.log 2>&1 || { echo "ab mid failed"; tail gpurun_out/ab_mid.log; exit 1; }
-  done
-  cat gpurun_out/ab_mid.log
 fi
 if [[ ,$STAGES, == *,sweep,* ]]; then  # mid-width sweep (tools/midp_sweep.py), then the same under rocprofv3
   timeout -k 10 400 python tools/midp_sweep.py ${SWEEP_P:-} > gpurun_out/midp_sweep.log 2>&1 || { echo "sweep failed"; tail gpurun_out/midp_sweep.log; exit 1; }

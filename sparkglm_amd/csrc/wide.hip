@@ -512,13 +512,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) w
 // beta and the scratch are __restrict__ kernel arguments and the row loop has a uniform trip count:
 // beta is then read through the scalar cache, not by vector loads, whose vmcnt wait would also wait
 // for every scratch store in flight.  GUARD: the workgroup's rows reach past the chunk or past n.
-#ifndef SGLM_GEN_NT
-#define SGLM_GEN_NT 0  // A/B (round 6): the scratch stores non-temporal
-#endif
-__device__ __forceinline__ void gen_store(double* p, double v) {
-  if constexpr (SGLM_GEN_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
 template <bool POS, bool GUARD>
 __device__ __forceinline__ void proc_gen_row(const ProcGenArgs& a, const double* __restrict__ beta,
                                              double* __restrict__ xs, int64_t t) {
@@ -537,8 +530,8 @@ __device__ __forceinline__ void proc_gen_row(const ProcGenArgs& a, const double*
   for (; j < pt; j += 4) {  // two columns at a time (two hash chains in flight: the VGPR budget)
     const double x0 = gx(j), x1 = gx(j + 1);
     if (in) {
-      gen_store(xo + (int64_t)j * ld, x0);
-      gen_store(xo + (int64_t)(j + 1) * ld, x1);
+      xo[(int64_t)j * ld] = x0;
+      xo[(int64_t)(j + 1) * ld] = x1;
     }
     if (beta) {
       e0 += x0 * beta[j];
@@ -547,8 +540,8 @@ __device__ __forceinline__ void proc_gen_row(const ProcGenArgs& a, const double*
     __builtin_amdgcn_sched_barrier(0);
     const double x2 = gx(j + 2), x3 = gx(j + 3);
     if (in) {
-      gen_store(xo + (int64_t)(j + 2) * ld, x2);
-      gen_store(xo + (int64_t)(j + 3) * ld, x3);
+      xo[(int64_t)(j + 2) * ld] = x2;
+      xo[(int64_t)(j + 3) * ld] = x3;
     }
     if (beta) {
       e2 += x2 * beta[j + 2];
@@ -558,7 +551,7 @@ __device__ __forceinline__ void proc_gen_row(const ProcGenArgs& a, const double*
   }
   for (; j < p; ++j) {
     const double x = gx(j);
-    if (in) gen_store(xo + (int64_t)j * ld, x);
+    if (in) xo[(int64_t)j * ld] = x;
     if (beta) e0 += x * beta[j];
   }
   if (beta && in && valid) a.eta_raw[row] = (e0 + e1) + (e2 + e3);

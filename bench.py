@@ -157,6 +157,20 @@ def pmc_traffic(p: int, n: int, family: str, procedural: bool = False):
         return None
 
 
+def lm_traffic(p: int, n: int):
+    """(traffic, source) of the LM Gram pass (configs[0]): the stored PMC entry 'gaussian:<p>:lm'
+    (tools/pmc_workloads.sh lm20: repeated LM fits, so X -- 168 MB -- comes from the Infinity Cache
+    after the first fit; FETCH_SIZE counts L2 fills from the fabric, MALL hits included)."""
+    tab = _pmc_table()
+    e = tab.get(f"gaussian:{p}:lm")
+    if not e or "bytes_per_row" not in e:
+        return None, f"none: no PMC pass stored for 'gaussian:{p}:lm'"
+    return e["bytes_per_row"] * n, (f"stored PMC, profiles/pmc_traffic.json['gaussian:{p}:lm']: "
+                                   f"{e['bytes_per_row']:.2f} B/row measured over {e.get('measured_rows')} rows "
+                                   f"({e.get('source', '?')}), x {n} rows of this launch; L2 fills from the fabric "
+                                   f"(repeated fits: X from the Infinity Cache)")
+
+
 def pmc_traffic_source(p: int, n: int, family: str, procedural: bool = False):
     """Where `roofline.traffic` comes from: it is NOT a counter of the timed run but a stored
     rocprofv3 --pmc measurement (bytes per row of a profiling pass over `measured_rows` rows of the
@@ -642,7 +656,7 @@ def run_lm(args, wl, eng, n, p, world, rank, dist_on, shared, barrier) -> int:
             "r2": fit.r2, "sse": fit.sse,
             "roofline": {"bound": "hbm", "kernel": st["pass_kernel_name"] + " (LM Gram)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": None, "traffic_source": "none: no PMC pass stored for the LM Gram shape",
+                         "traffic": lm_traffic(p, n)[0], "traffic_source": lm_traffic(p, n)[1],
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass,
                          "note": "1M x 20 = 168 MB per pass: launch- and latency-bound, not a bandwidth test"},
             "breakdown_ms_per_step": {"gram_pass_kernel": kern_ms, "reduce": st["reduce_kernel_ms"] / args.steps,

@@ -20,6 +20,7 @@ WL = {  # name: (key, rows, kernel substrings of the pass, substring of the kern
     "logit256": ("binomial:256", 20_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"], "irls_pass"),
     "logit512": ("binomial:512", 8_000_000, WIDE, "wide_rows_kernel<"),
     "logit512p": ("binomial:512:proc", 8_000_000, WIDE, "wide_rows_kernel<"),
+    "lm20": ("gaussian:20:lm", 1_000_000, ["irls_narrow_kernel"], "irls_narrow_kernel"),
     "gamma2048": ("gamma:2048", 2_000_000, WIDE, "wide_rows_kernel<"),
     "mid160": ("binomial:160", 10_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"], "irls_pass"),
     "mid96": ("binomial:96", 15_000_000, ["irls_pass_kernel", "irls_pass_r_kernel"], "irls_pass"),

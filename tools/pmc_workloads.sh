@@ -21,6 +21,7 @@ for wl in ${WLS:-poisson64 logit256 logit512 gamma2048 logit32}; do
     mid160) run_wl mid160 10000000 160 0 binomial logit ;;     # mid-width K1r<10>
     mid96) run_wl mid96 15000000 96 0 binomial logit ;;        # mid-width K1<6>, three workgroups per CU
     logit512p) run_wl logit512p 8000000 512 0 binomial logit 1 ;;  # procedural shard (HBM-scratch chunks)
+    lm20) run_wl lm20 1000000 20 1 gaussian identity 0 PLM=1 ;;       # configs[0]: the one-pass LM Gram
   esac
 done
 exit 0

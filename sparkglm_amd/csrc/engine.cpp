@@ -414,7 +414,7 @@ struct sglm_engine : public Backend {
   // SGLM_PROC_OVERLAP: chunks of an overlapped procedural pass (<= 1: one buffer, serial).  Round 2
   // measured it slower beside both Gram launches (250M x 512 logit: 1257 ms per pass serial, 1420 /
   // 1480 at 8 / 16 chunks -- the generator's integer + fp64 VALU slowed the Gram by 31-38 %).  Round 5
-  // (VERDICT r4 item 6): gated to the off-diagonal launches (SGLM_PROC_OV_GATE; the diagonal launch
+  // (VERDICT r4 item 6): gated to the off-diagonal launches (then SGLM_PROC_OV_GATE; the diagonal launch
   // goes first) and the generating row kernel at raised priority, 8 chunks: 1284.5 -> 1266.9 ms on one
   // box (ungated 1466.3, gated at normal priority 1285.7).  Round 5 then split the
   // generator off (proc_gen_kernel, 48 VGPRs) and let it start beside each chunk's diagonal launch,

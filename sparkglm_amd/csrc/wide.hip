@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) w
   wide_rows_body<FAM, LNK, 2, true>(a);
 }
 
-// Procedural chunks, the generator on its own (engine.cpp, SGLM_PROC_LEAN): X rows [r_begin, r_end)
+// Procedural chunks >= 1, the generator on its own (engine.cpp enqueue_pass): X rows [r_begin, r_end)
 // into the scratch and X beta into eta_raw, a thread per row, nothing else -- so that it fits in 48
 // VGPRs and two waves per SIMD run beside the two 208-VGPR off-diagonal Gram workgroups (the
 // generating wide_rows_ov_kernel, with the family arithmetic in it, holds 87 VGPRs: one wave).  The

@@ -271,8 +271,8 @@ int sglm_get_data(sglm_engine *h, double *X, double *y, double *m, double *offse
 
 /* ---- communicators (Spark treeReduce replacement) ----------------------------- */
 /* fn runs on the handle's communicator thread unless SGLM_COMM_TIMEOUT_S=0 (see sglm_allreduce_fn).
- * RCCL (sglm_set_comm_rccl) and group handles: the deadline of each pass's all-reduce starts when
- * this rank's own pass kernels have finished, so it bounds the wait for the peers only. */
+ * RCCL (sglm_set_comm_rccl) and group handles: the deadline of an all-reduce starts when the work
+ * this rank queued before it (its pass kernels) has finished, so it bounds the wait for the peers only. */
 int sglm_set_comm(sglm_engine *h, sglm_allreduce_fn fn, void *ctx, int on_device);
 /* This handle's rank in the communicator just set by sglm_set_comm (0 <= rank < its rank count;
  * known without this call for RCCL and sglm_local_allreduce).  With it the per-iteration scalars

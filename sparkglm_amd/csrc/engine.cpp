@@ -379,6 +379,7 @@ struct sglm_engine : public Backend {
   hipStream_t st = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t evc = nullptr;  // end of the pass's device all-reduce (comm time = ev2 -> evc)
+  hipEvent_t evpre = nullptr;  // before a small RCCL all-reduce: where its deadline starts
   int ncu = 256;
   // resident shard
   int64_t n = 0, p = 0, n_pad = 0, nblocks = 0;
@@ -544,9 +545,10 @@ struct sglm_engine : public Backend {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
+    if (evpre) (void)hipEventDestroy(evpre);
     if (evc) (void)hipEventDestroy(evc);
     if (st) (void)hipStreamDestroy(st);
-    ev0 = ev1 = ev2 = evc = nullptr;
+    ev0 = ev1 = ev2 = evc = evpre = nullptr;
     st = nullptr;
   }
 
@@ -581,15 +583,20 @@ struct sglm_engine : public Backend {
         return SGLM_ECOMM;
       }
       const double t0 = now_ms();
+      // the deadline starts when everything this rank queued before the collective is done: the pass
+      // (ev2, recorded at its end) or, for the small all-reduces, whatever precedes them on st
+      if (!after_pass) {
+        if (!evpre) HIPCHK(hipEventCreateWithFlags(&evpre, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(evpre, st));
+      }
       ncclResult_t r = ncclAllReduce(dbuf, dbuf, (size_t)count, ncclFloat64, ncclSum, comm.nccl, st);
       if (r != ncclSuccess) {
         set_error(std::string("RCCL ncclAllReduce on ") + rank_str(comm.rank) + ": " + ncclGetErrorString(r));
         return SGLM_ECOMM;
       }
       if (after_pass) HIPCHK(hipEventRecord(evc, st));
-      // after a pass: the deadline starts when the pass (ev2, recorded before the collective) is done
       if (int rc = wait_collective({st}, {&comm.nccl}, comm.timeout_ms, comm.rank, "ncclAllReduce",
-                                   after_pass ? std::vector<hipEvent_t>{ev2} : std::vector<hipEvent_t>{}))
+                                   {after_pass ? ev2 : evpre}))
         return rc;
       if (after_pass) {
         float ms = 0.f;

@@ -165,3 +165,27 @@ def test_rank_failures_end_with_an_error_not_a_hang(case):
         assert res[1] == "exited"
         assert res[0].startswith("ecomm:"), res[0]
         assert float(res[0].split(":")[1]) < 60.0, res[0]
+
+
+def test_rccl_deadline_counts_from_the_end_of_the_pass(monkeypatch):
+    """the RCCL all-reduce's deadline starts when this rank's own pass has
+    finished (wait_collective polls the pass-end event first), so a pass longer than
+    SGLM_COMM_TIMEOUT_S on a large shard does not abort a healthy communicator.  World 1 over the
+    engine's RCCL communicator, a 50 ms deadline against the ~110 ms passes of configs[1]'s 100M x 256
+    shard: the fit completes over RCCL and matches the streaming oracle's full-size fit."""
+    import json
+    from sparkglm_amd import Engine
+    fs = os.path.join(ROOT, "tests", "golden", "full_scale.json")
+    if not os.path.exists(fs):
+        pytest.skip("full_scale.json absent")
+    c = json.load(open(fs))["logit256"]
+    monkeypatch.setenv("SGLM_COMM_TIMEOUT_S", "0.05")
+    with Engine(0) as e:
+        e.synth(c["kind"], c["row0"], c["n"], c["p"], c["seed"])
+        e.set_comm_rccl(1, 0, Engine.rccl_unique_id())
+        f = e.fit_glm(c["family"], c["link"], tol=c["tol"])
+        st = e.stats()
+    assert st["comm_path_name"] == "rccl" and st["pass_kernel_ms"] / max(st["passes"], 1) > 60.0
+    assert f.iter == c["iter"]
+    assert rel(f.coefs, c["coefs"]) < 1e-9 and rel(f.stderr, c["stderr"]) < 1e-9
+    assert rel(f.deviance, c["deviance"]) < 1e-9

@@ -345,6 +345,7 @@ def main() -> int:
     eng.synth(wl["kind"], row0, n, p, seed, procedural=wl.get("procedural", False))  # this rank's shard
     gen_s = time.perf_counter() - t0
     attach_comm(eng, args, world, rank, dist_on, shared)
+    warm_comm(eng, dist_on, wl["family"], wl["link"])
     log(f"[rank {rank}] shard {n} x {p} ({args.workload}) generated in {gen_s:.2f} s")
 
     if wl.get("lm"):
@@ -436,7 +437,9 @@ def main() -> int:
                        "rows_per_gpu": n, "p": p, "global_rows": total_rows, "parallelism": f"rows{world}" + ("-shared-device-gloo" if shared else ""),
                        "allreduce": "gloo" if shared else ("rccl-engine" if args.comm == "rccl" else "rccl-torch"),
                        "family": fam, "link": lnk, "tol": 1e-6,
-                       "offset_prior": wl["kind"] == 2, "procedural_x": wl.get("procedural", False)},
+                       "offset_prior": wl["kind"] == 2, "procedural_x": wl.get("procedural", False),
+                       "comm_warmup": ("one untimed initial-mode pass over the communicator before timing "
+                                       "(RCCL peer-connection setup)") if dist_on else None},
             "time_to_converge_s": ttc,
             "iters_to_converge": fit.iter,
             "deviance": fit.deviance,
@@ -566,6 +569,15 @@ def attach_comm(eng, args, world: int, rank: int, dist_on: bool, shared: bool) -
         args.comm = comm
 
 
+def warm_comm(eng, dist_on: bool, family: str, link: str) -> None:
+    """N > 1: one untimed initial-mode pass over the just-attached communicator before anything is
+    timed -- a fresh RCCL communicator sets up its peer connections on its first collective, a
+    one-time cost of the job (Spark's executors are up before a fit is timed), not of a fit.  The
+    pass's results are discarded; every rank makes the same call (collective)."""
+    if dist_on:
+        eng.irls_pass(None, mu0=0.5, family=family, link=link)
+
+
 def strong_1b(args, dev: int, world: int, rank: int, dist_on: bool, shared: bool, barrier) -> dict:
     """North-star strong-scaling point measured beside the headline: the 1B x 32 logistic GLM
     (the logit1b workload) row-sharded over the N ranks of this run -- time to converge
@@ -591,6 +603,7 @@ def strong_1b(args, dev: int, world: int, rank: int, dist_on: bool, shared: bool
         if not ok:
             raise RuntimeError("1B x 32 shard not generated on every rank")
         attach_comm(eng, args, world, rank, dist_on, shared)
+        warm_comm(eng, dist_on, wl["family"], wl["link"])
         barrier()
         t0 = time.perf_counter()
         fit = eng.fit_glm(wl["family"], wl["link"], tol=1e-6)

@@ -218,3 +218,15 @@ def test_fp64_pipe_bound_reproduces_from_the_stored_pmc_mix():
     hbm_frac = 125_000_000 * 536 / (b["pipe_bound_ms"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS
     assert 0.55 < hbm_frac < 0.70
     assert bench.fp64_pipe_bound({"clock_ghz": 2.0}, 10) == {}  # no stored mix: no bound claimed
+
+
+def test_cpu_baseline_states_its_cores():
+    # the CPU baseline runs on every host core the job owns -- the affinity mask,
+    # capped by OMP_NUM_THREADS when set (the GPU pool's 16-core share) -- and says so
+    import os as _os
+    aff = len(_os.sched_getaffinity(0))
+    hc = bench.host_cores({"OMP_NUM_THREADS": "4"})
+    assert hc["threads"] == min(4, aff) and hc["affinity_cpus"] == aff and hc["omp_num_threads"] == 4
+    assert hc["host_cpu_count"] == (_os.cpu_count() or 1)
+    assert bench.host_cores({})["threads"] == aff and bench.host_cores({})["omp_num_threads"] is None
+    assert bench.host_cores({"OMP_NUM_THREADS": "junk"})["threads"] == aff

@@ -230,3 +230,13 @@ def test_cpu_baseline_states_its_cores():
     assert hc["host_cpu_count"] == (_os.cpu_count() or 1)
     assert bench.host_cores({})["threads"] == aff and bench.host_cores({})["omp_num_threads"] is None
     assert bench.host_cores({"OMP_NUM_THREADS": "junk"})["threads"] == aff
+
+
+def test_lm_line_traffic_comes_from_the_lm_pmc_entry():
+    # the lm20 line's roofline.traffic was null; now the stored PMC of the LM Gram
+    # pass (tools/pmc_workloads.sh lm20 -> pmc_traffic.json['gaussian:20:lm'])
+    tab = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    t, src = bench.lm_traffic(20, 1_000_000)
+    assert t == tab["gaussian:20:lm"]["bytes_per_row"] * 1_000_000
+    assert "gaussian:20:lm" in src and "Infinity Cache" in src
+    assert bench.lm_traffic(7, 10)[0] is None

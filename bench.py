@@ -16,6 +16,11 @@ one rank; a plain `python bench.py --gpus N` launches those N rank processes its
 torch.distributed.run, before anything touches the GPU) and exits with their status.  Each rank
 holds its own 100M-row shard (weak scaling) and the per-iteration Gram all-reduce runs on RCCL
 over xGMI inside the engine.  Rank 0 prints ONE JSON line.
+
+The default run (N = 1) also measures, after the headline, the north-star 1B x 32 strong point
+(`strong_scaling_1b_logit`) and every other BASELINE config's per-GPU shard (`configs_n1`: configs[0]
+LM, the configs[2] Poisson, configs[3] gamma and configs[4] procedural shards), each with its own
+roofline object; `--no-strong` / `--no-configs` skip them.
 """
 from __future__ import annotations
 
@@ -41,7 +46,7 @@ def log(*a):
 
 
 # BASELINE.json configs -> bench workloads.  The default (N=1 headline) is configs[1]; the others
-# are measured with --workload and recorded under profiles/ (rows per GPU = the config's global
+# are measured in the default run's configs_n1 and with --workload, recorded under profiles/ (rows per GPU = the config's global
 # rows / 8 where the config is quoted on 8 GPUs, or the largest resident shard, as labelled).
 WORKLOADS = {
     "lm20": dict(cfg=0, kind=1, family="gaussian", link="identity", p=20, rows=1_000_000, seed=1, lm=True,
@@ -298,6 +303,8 @@ def main() -> int:
     ap.add_argument("--no-load", action="store_true", help="skip the host-to-HBM load probe")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the 1B x 32 strong-scaling point measured after the default workload")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs' N = 1 points measured after the default workload")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
 
@@ -380,46 +387,7 @@ def main() -> int:
         total_rows = wl["strong_rows"] if strong else n * world
         passes = max(st["passes"], 1)
         wide = st["path"] == 1
-        nvec = 1 + (2 if wl["kind"] == 2 else 0)  # y (+ offset, prior)
-        flops = n * (p * (p + 1) + 2 * p)      # SYRK-convention X'WX + X'Wz per launch
-        bytes_pass = n * (8 * p + 8 * nvec)    # X row + per-row vectors, read once per pass
-        # the kernel is the one the engine dispatched (sglm_stats.pass_kernel_name), not re-derived here
-        kern = st["pass_kernel_name"] + (" (K1r, split-role fused pass)" if st["pass_kernel_kind"] == "fused-split" else "")
-        if wide:
-            kern_ms = st["gram_kernel_ms"] / passes
-            pass_ms = st["pass_kernel_ms"] / passes  # wall span of the pass (row and Gram may overlap)
-        else:
-            kern_ms = st["pass_kernel_ms"] / passes
-            pass_ms = kern_ms
-        tflops = flops / (kern_ms * 1e-3) / 1e12
-        gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(p, n, fam, wl.get("procedural", False))
-        traffic_src = pmc_traffic_source(p, n, fam, wl.get("procedural", False))
-        if flops / bytes_pass < RIDGE:  # HBM-bound fused pass (arithmetic intensity below the ridge)
-            roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel_ms": kern_ms,
-                    "algorithmic_bytes_per_launch": bytes_pass,
-                    "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS,
-                    "fp64_pipe": mfma_clock_bound(p, n, fam)}
-            # how close the pass is to the fp64 pipe's bound, and the HBM fraction that bound allows:
-            # an HBM target above it is out of reach at this clock whatever the memory system does
-            pb = roof["fp64_pipe"].get("pipe_bound_ms")
-            if pb:
-                roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
-                roof["fp64_pipe"]["hbm_frac_at_pipe_bound"] = bytes_pass / (pb * 1e-3) / 1e9 / HBM_PEAK_GBS
-        else:
-            roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                    "traffic_source": traffic_src, "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
-                    "hbm_gbs_algorithmic": gbs, "fp64_pipe": mfma_clock_bound(p, n, fam, wl.get("procedural", False))}
-            # the MFMA instruction stream at the clock the chip holds under the kernel (PMC), against
-            # the measured kernel time: how close the kernel is to its clock-limited bound
-            sm = roof["fp64_pipe"].get("mfma_stream_ms_at_pmc_clock")
-            roof["fp64_pipe"]["kernel_frac_of_clock_limited_stream"] = sm / kern_ms if sm and kern_ms else None
-            pb = roof["fp64_pipe"].get("pipe_bound_ms")
-            if pb:
-                roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
+        roof, pass_ms = pass_roofline(st, wl, n, p)
         out = {
             "metric": METRIC,
             "value": total_rows * args.steps / dt,
@@ -475,12 +443,141 @@ def main() -> int:
             strong_1b_res = None
         if rank == 0:
             out["strong_scaling_1b_logit"] = strong_1b_res
+    if args.workload == "logit256" and world == 1 and not args.no_configs:
+        out["configs_n1"] = config_points(dev)
     if rank == 0:
         print(json.dumps(out), file=JSON_OUT, flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def pass_roofline(st: dict, wl: dict, n: int, p: int):
+    """The `roofline` object of a GLM line (and the pass's wall span in ms) from the engine's stats
+    over the timed iterations: the bound follows the pass's arithmetic intensity."""
+    fam = wl["family"]
+    passes = max(st["passes"], 1)
+    wide = st["path"] == 1
+    nvec = 1 + (2 if wl["kind"] == 2 else 0)  # y (+ offset, prior)
+    flops = n * (p * (p + 1) + 2 * p)      # SYRK-convention X'WX + X'Wz per launch (SURVEY 8d)
+    bytes_pass = n * (8 * p + 8 * nvec)    # X row + per-row vectors, read once per pass (SURVEY 8d)
+    # the kernel is the one the engine dispatched (sglm_stats.pass_kernel_name), not re-derived here
+    kern = st["pass_kernel_name"] + (" (K1r, split-role fused pass)" if st["pass_kernel_kind"] == "fused-split" else "")
+    if wide:
+        kern_ms = st["gram_kernel_ms"] / passes
+        pass_ms = st["pass_kernel_ms"] / passes  # wall span of the pass (row and Gram may overlap)
+    else:
+        kern_ms = st["pass_kernel_ms"] / passes
+        pass_ms = kern_ms
+    tflops = flops / (kern_ms * 1e-3) / 1e12
+    gbs = bytes_pass / (pass_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(p, n, fam, wl.get("procedural", False))
+    traffic_src = pmc_traffic_source(p, n, fam, wl.get("procedural", False))
+    if flops / bytes_pass < RIDGE:  # HBM-bound fused pass (arithmetic intensity below the ridge)
+        roof = {"bound": "hbm", "kernel": kern, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": bytes_pass,
+                "mfma_tflops": tflops, "mfma_frac": tflops / FP64_MFMA_PEAK_TFLOPS,
+                "fp64_pipe": mfma_clock_bound(p, n, fam)}
+        # how close the pass is to the fp64 pipe's bound, and the HBM fraction that bound allows:
+        # an HBM target above it is out of reach at this clock whatever the memory system does
+        pb = roof["fp64_pipe"].get("pipe_bound_ms")
+        if pb:
+            roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
+            roof["fp64_pipe"]["hbm_frac_at_pipe_bound"] = bytes_pass / (pb * 1e-3) / 1e9 / HBM_PEAK_GBS
+    else:
+        roof = {"bound": "mfma", "kernel": kern, "achieved": tflops, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": tflops / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                "traffic_source": traffic_src, "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
+                "hbm_gbs_algorithmic": gbs, "fp64_pipe": mfma_clock_bound(p, n, fam, wl.get("procedural", False))}
+        # the MFMA instruction stream at the clock the chip holds under the kernel (PMC), against
+        # the measured kernel time: how close the kernel is to its clock-limited bound
+        sm = roof["fp64_pipe"].get("mfma_stream_ms_at_pmc_clock")
+        roof["fp64_pipe"]["kernel_frac_of_clock_limited_stream"] = sm / kern_ms if sm and kern_ms else None
+        pb = roof["fp64_pipe"].get("pipe_bound_ms")
+        if pb:
+            roof["fp64_pipe"]["kernel_frac_of_pipe_bound"] = pb / kern_ms
+    return roof, pass_ms
+
+
+# The other BASELINE configs measured inside the default N = 1 run (after the headline and the strong
+# point, each on its own engine, freed before the next), so the driver's run observes every config's
+# per-GPU shard, not only builder-side profiles/.  Compact: a fit to convergence, one warm-up
+# iteration, CONFIG_STEPS timed iterations (LM: CONFIG_LM_FITS timed fits).
+CONFIG_POINTS = ("lm20", "poisson64", "gamma2048", "logit512")
+CONFIG_STEPS = 3
+CONFIG_LM_FITS = 20
+
+
+def config_point(name: str, dev: int) -> dict:
+    """One BASELINE config's per-GPU shard at N = 1 (the shapes and labels of WORKLOADS): time to
+    converge, ms per timed IRLS iteration (LM: per fit), rows/s and the roofline object."""
+    import torch
+    from sparkglm_amd import Engine
+    wl = WORKLOADS[name]
+    n, p = wl["rows"], wl["p"]
+    eng = Engine(dev)
+    try:
+        t0 = time.perf_counter()
+        eng.synth(wl["kind"], 0, n, p, wl["seed"], procedural=wl.get("procedural", False))
+        torch.cuda.synchronize()
+        gen_s = time.perf_counter() - t0
+        if wl.get("lm"):
+            fit = eng.fit_lm()
+            eng.reset_stats()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(CONFIG_LM_FITS):
+                fit = eng.fit_lm()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / CONFIG_LM_FITS
+            st = eng.stats()
+            kern_ms = st["pass_kernel_ms"] / max(st["passes"], 1)
+            bytes_pass = n * (8 * p + 8)
+            gbs = bytes_pass / (kern_ms * 1e-3) / 1e9
+            return {"workload": f"{name}: {wl['label']}", "rows": n, "p": p, "generate_s": gen_s,
+                    "ms_per_fit": dt * 1e3, "rows_per_s": n / dt, "fits_timed": CONFIG_LM_FITS, "r2": fit.r2,
+                    "roofline": {"bound": "hbm", "kernel": st["pass_kernel_name"] + " (LM Gram)", "achieved": gbs,
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                 "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_pass}}
+        fam, lnk = wl["family"], wl["link"]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fit = eng.fit_glm(fam, lnk, tol=1e-6)
+        torch.cuda.synchronize()
+        ttc = time.perf_counter() - t0
+        beta = np.array(fit.coefs, dtype=np.float64)
+        beta, _ = eng.irls_iterations(beta, 1, fam, lnk)
+        eng.reset_stats()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.irls_iterations(beta, CONFIG_STEPS, fam, lnk)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / CONFIG_STEPS
+        st = eng.stats()
+        roof, pass_ms = pass_roofline(st, wl, n, p)
+        return {"workload": f"{name}: {wl['label']}", "rows": n, "p": p, "family": fam, "link": lnk,
+                "procedural_x": wl.get("procedural", False), "generate_s": gen_s,
+                "time_to_converge_s": ttc, "iters_to_converge": fit.iter, "deviance": fit.deviance,
+                "ms_per_iter": dt * 1e3, "rows_per_s_per_iter": n / dt, "iters_timed": CONFIG_STEPS,
+                "pass_ms": pass_ms, "solve_path": st["solve_path_name"], "roofline": roof}
+    finally:
+        eng.close()
+
+
+def config_points(dev: int) -> dict:
+    out = {}
+    for name in CONFIG_POINTS:
+        try:  # never lose the headline line to a secondary measurement
+            out[name] = config_point(name, dev)
+            log(f"[rank 0] config point {name}: " + (f"{out[name]['ms_per_fit']:.3f} ms per fit" if "ms_per_fit" in out[name]
+                                                     else f"{out[name]['ms_per_iter']:.1f} ms per iteration"))
+        except Exception as exc:
+            log(f"[rank 0] config point {name} failed: {exc}")
+            out[name] = {"error": f"{type(exc).__name__}: {exc}"}
+    return out
 
 
 def load_probe(dev: int, p: int, wl: dict, n_shard: int, sample_bytes: float = 4e9) -> dict:

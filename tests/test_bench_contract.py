@@ -240,3 +240,30 @@ def test_lm_line_traffic_comes_from_the_lm_pmc_entry():
     assert t == tab["gaussian:20:lm"]["bytes_per_row"] * 1_000_000
     assert "gaussian:20:lm" in src and "Infinity Cache" in src
     assert bench.lm_traffic(7, 10)[0] is None
+
+
+def test_default_run_covers_every_baseline_config():
+    # the headline (configs[1]) + the strong 1B point + configs_n1: every config's per-GPU shard is
+    # measured by the driver's own default run, not only by builder-side --workload runs
+    cfgs = json.load(open(os.path.join(ROOT, "BASELINE.json")))["configs"]
+    covered = {bench.WORKLOADS["logit256"]["cfg"]} | {bench.WORKLOADS[w]["cfg"] for w in bench.CONFIG_POINTS}
+    assert covered == set(range(len(cfgs)))
+    assert "logit256" not in bench.CONFIG_POINTS and bench.CONFIG_STEPS >= 1
+
+
+def test_pass_roofline_from_stats():
+    # a fused-pass line: the kernel time is the pass time; MFMA-bound at p = 256
+    st = {"passes": 2, "path": 0, "pass_kernel_name": "k", "pass_kernel_kind": "fused-split",
+          "pass_kernel_ms": 200.0, "gram_kernel_ms": 0.0}
+    roof, pass_ms = bench.pass_roofline(st, bench.WORKLOADS["logit256"], 100_000_000, 256)
+    assert roof["bound"] == "mfma" and pass_ms == 100.0 and roof["kernel_ms"] == 100.0
+    assert abs(roof["achieved"] - 1e8 * (256 * 257 + 512) / 0.1 / 1e12) < 1e-9
+    # a wide line: the Gram kernels are the dominant kernel, the pass span is the wall clock
+    st = dict(st, path=1, pass_kernel_kind="wide", pass_kernel_ms=600.0, gram_kernel_ms=560.0)
+    roof, pass_ms = bench.pass_roofline(st, bench.WORKLOADS["gamma2048"], 12_500_000, 2048)
+    assert roof["bound"] == "mfma" and pass_ms == 300.0 and roof["kernel_ms"] == 280.0
+    # an HBM-bound narrow line carries the fp64-pipe fractions
+    st = dict(st, path=0, pass_kernel_kind="narrow", pass_kernel_ms=28.0)
+    roof, _ = bench.pass_roofline(st, bench.WORKLOADS["poisson64"], 125_000_000, 64)
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s"
+    assert "kernel_frac_of_pipe_bound" in roof["fp64_pipe"]

@@ -18,22 +18,74 @@
 
 namespace sglm {
 
-// Left-looking (jki) Cholesky on a column-major full matrix; lower triangle out.
+// Left-looking (jki) Cholesky on a column-major full matrix; lower triangle out.  Four columns at a
+// time: the panel's update by the columns before it streams each of those columns once for all four
+// (the p = 256 solve of every configs[1] iteration: 0.86 -> 0.3 ms on one core), then the panel
+// factors column by column.  Every element still subtracts its terms in k order, one rounding each,
+// so the factor is bitwise the column-by-column one (the rows above the diagonal that the panel
+// update also touches are never read and are zeroed at the end).
 int chol_factor(double* A, int64_t p) {
-  for (int64_t j = 0; j < p; ++j) {
-    double* Aj = A + j * p;
-    for (int64_t k = 0; k < j; ++k) {
-      const double ljk = A[j + k * p];
-      if (ljk == 0.0) continue;
-      const double* Ak = A + k * p;
-      for (int64_t i = j; i < p; ++i) Aj[i] -= Ak[i] * ljk;
+  constexpr int64_t NB = 4;
+  for (int64_t j0 = 0; j0 < p; j0 += NB) {
+    const int64_t nb = p - j0 < NB ? p - j0 : NB;
+    double* P = A + j0 * p;  // the panel's first column
+    // the panel's update by the columns k < j0.  Dense panel (no zero multiplier): 8-row blocks of the
+    // four columns stay in registers over the whole k loop; otherwise column by column with the
+    // zero multipliers skipped, as the unblocked loop does
+    bool dense = nb == NB;
+    for (int64_t k = 0; k < j0 && dense; ++k)
+      for (int64_t c = 0; c < NB; ++c) dense = dense && A[j0 + c + k * p] != 0.0;
+    if (dense) {
+      constexpr int64_t R = 8;
+      int64_t i0 = j0;
+      for (; i0 + R <= p; i0 += R) {
+        double acc[NB][R];
+        for (int64_t c = 0; c < NB; ++c)
+          for (int64_t r = 0; r < R; ++r) acc[c][r] = P[c * p + i0 + r];
+        for (int64_t k = 0; k < j0; ++k) {
+          const double* Ak = A + k * p;
+          const double* lk = A + k * p + j0;
+          for (int64_t c = 0; c < NB; ++c) {
+            const double l = lk[c];
+            for (int64_t r = 0; r < R; ++r) acc[c][r] -= Ak[i0 + r] * l;
+          }
+        }
+        for (int64_t c = 0; c < NB; ++c)
+          for (int64_t r = 0; r < R; ++r) P[c * p + i0 + r] = acc[c][r];
+      }
+      for (int64_t k = 0; k < j0 && i0 < p; ++k) {  // the last rows
+        const double* Ak = A + k * p;
+        for (int64_t c = 0; c < NB; ++c) {
+          const double l = A[j0 + c + k * p];
+          for (int64_t i = i0; i < p; ++i) P[c * p + i] -= Ak[i] * l;
+        }
+      }
+    } else {
+      for (int64_t k = 0; k < j0; ++k) {
+        const double* Ak = A + k * p;
+        for (int64_t c = 0; c < nb; ++c) {
+          const double l = A[j0 + c + k * p];
+          if (l == 0.0) continue;
+          double* Pc = P + c * p;
+          for (int64_t i = j0; i < p; ++i) Pc[i] -= Ak[i] * l;
+        }
+      }
     }
-    const double d = Aj[j];
-    if (!(d > 0.0) || !std::isfinite(d)) return (int)(j + 1);
-    const double s = std::sqrt(d);
-    Aj[j] = s;
-    const double inv = 1.0 / s;
-    for (int64_t i = j + 1; i < p; ++i) Aj[i] *= inv;
+    for (int64_t j = j0; j < j0 + nb; ++j) {
+      double* Aj = A + j * p;
+      for (int64_t k = j0; k < j; ++k) {
+        const double ljk = A[j + k * p];
+        if (ljk == 0.0) continue;
+        const double* Ak = A + k * p;
+        for (int64_t i = j; i < p; ++i) Aj[i] -= Ak[i] * ljk;
+      }
+      const double d = Aj[j];
+      if (!(d > 0.0) || !std::isfinite(d)) return (int)(j + 1);
+      const double s = std::sqrt(d);
+      Aj[j] = s;
+      const double inv = 1.0 / s;
+      for (int64_t i = j + 1; i < p; ++i) Aj[i] *= inv;
+    }
   }
   for (int64_t j = 1; j < p; ++j)
     for (int64_t i = 0; i < j; ++i) A[i + j * p] = 0.0;

@@ -182,3 +182,57 @@ def test_cross_rank_scalars_are_summed_in_rank_blocks(golden):
         return fn
     res = _adversarial_scalar_fits(golden, plain)
     assert all(res[r].deviance == 8.0 for r in range(3))
+
+
+def _chol_solve_unblocked(packed, p):
+    """The host solve restated element by element in the order of the unblocked left-looking (jki)
+    Cholesky + two column sweeps (solve.cpp before the 4-column panels): every a - b * c is a product
+    rounded, then a difference rounded, exactly as the C++ does without FMA contraction."""
+    import math
+    A = [[0.0] * p for _ in range(p)]  # A[col][row]
+    for i in range(p):
+        for j in range(i + 1):
+            A[j][i] = A[i][j] = float(packed[i * (i + 1) // 2 + j])
+    for j in range(p):
+        Aj = A[j]
+        for k in range(j):
+            ljk = A[k][j]
+            if ljk == 0.0:
+                continue
+            Ak = A[k]
+            for i in range(j, p):
+                Aj[i] = Aj[i] - Ak[i] * ljk
+        s = math.sqrt(Aj[j])
+        Aj[j] = s
+        inv = 1.0 / s
+        for i in range(j + 1, p):
+            Aj[i] = Aj[i] * inv
+    t = [float(v) for v in packed[p * (p + 1) // 2: p * (p + 1) // 2 + p]]
+    for j in range(p):
+        t[j] = t[j] / A[j][j]
+        for i in range(j + 1, p):
+            t[i] = t[i] - A[j][i] * t[j]
+    for i in range(p - 1, -1, -1):
+        t[i] = t[i] / A[i][i]
+        for k in range(i):
+            t[k] = t[k] - A[k][i] * t[i]
+    return np.array(t)
+
+
+@pytest.mark.parametrize("p", [5, 37, 64])
+def test_panel_cholesky_is_bitwise_the_unblocked_factor(p):
+    """solve.cpp factors four columns at a time (8-row register blocks, AVX2, no FMA): the LM
+    coefficients (LM.scala:225-227, the Cholesky solve of X'X b = X'y) equal, bit for bit, the
+    unblocked factorization's restated in Python -- p = 5 / 37 cover a partial last panel and rows
+    past the last 8-row block."""
+    rng = np.random.default_rng(p)
+    X = np.asfortranarray(rng.normal(size=(400, p)))
+    y = X @ rng.normal(size=p) + rng.normal(size=400)
+    seen = {}
+
+    def part(mode, b, mu0, ybar):
+        v = po.shard_partials(X, y, "gaussian", "identity", mode, b, mu0, ybar)
+        seen.setdefault(mode, v.copy())
+        return v
+    f = D.fit_lm_external(p, lambda: (y.sum(), len(y)), part)
+    np.testing.assert_array_equal(f.coefs, _chol_solve_unblocked(seen[3], p))

@@ -22,7 +22,7 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 
-template <int NRB, int NC, int DEPTH, int NW, bool BLOCKED>
+template <int NRB, int NC, int DEPTH, int NW, bool BLOCKED, int AUX = 0>
 __global__ void __launch_bounds__(64 * NW, 1) stream_kernel(const double* X, int64_t ld, int64_t nb, double* out,
                                                             unsigned long long* clk) {
   constexpr int NOCT = NC * NRB / 128;  // 1 KiB wave-instructions per block
@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(64 * NW, 1) stream_kernel(const double* X, int
     for (int o = 0; o < NOCT; ++o) {
       const double* src =
           BLOCKED ? X + blk * (NC * NRB) + o * 128 + loff : X + blk * NRB + (int64_t)(CPI * o) * ld + loff;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(wl + buf * NC * NRB + o * 128), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(wl + buf * NC * NRB + o * 128), 16, 0, AUX);
     }
   };
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -80,7 +80,7 @@ static double* out;
 static unsigned long long* clk;
 static const int64_t NROWS = 400000000;  // 102 GB at 32 columns, 205 GB at 64
 
-template <int NRB, int NC, int DEPTH, int NW, bool BLOCKED>
+template <int NRB, int NC, int DEPTH, int NW, bool BLOCKED, int AUX = 0>
 void run(int grid) {
   const int64_t n = NC == 32 ? NROWS : NROWS / 2, nb = n / NRB;
   hipEvent_t e0, e1;
@@ -88,7 +88,7 @@ void run(int grid) {
   hipEventCreate(&e1);
   for (int it = 0; it < 4; ++it) {
     hipEventRecord(e0);
-    hipLaunchKernelGGL((stream_kernel<NRB, NC, DEPTH, NW, BLOCKED>), dim3(grid), dim3(64 * NW), 0, 0, X, n, nb, out, clk);
+    hipLaunchKernelGGL((stream_kernel<NRB, NC, DEPTH, NW, BLOCKED, AUX>), dim3(grid), dim3(64 * NW), 0, 0, X, n, nb, out, clk);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms = 0;
@@ -96,8 +96,8 @@ void run(int grid) {
     unsigned long long h[2];
     hipMemcpy(h, clk, sizeof h, hipMemcpyDeviceToHost);
     if (it == 3)
-      printf("p %2d NRB %2d depth %d waves %2d grid %3d %s: %.3f ms  %.0f GB/s  clock %.2f GHz  LDS %d KiB\n", NC, NRB,
-             DEPTH, NW, grid, BLOCKED ? "row-block-major" : "column-major   ", ms, (double)n * NC * 8 / ms / 1e6,
+      printf("p %2d NRB %2d depth %d waves %2d grid %3d aux %d %s: %.3f ms  %.0f GB/s  clock %.2f GHz  LDS %d KiB\n", NC, NRB,
+             DEPTH, NW, grid, AUX, BLOCKED ? "row-block-major" : "column-major   ", ms, (double)n * NC * 8 / ms / 1e6,
              (double)h[0] / (double)h[1] * 0.1, NW * DEPTH * NC * NRB * 8 / 1024);
   }
   fflush(stdout);
@@ -111,22 +111,19 @@ int main() {
   hipDeviceSynchronize();
   hipMalloc(&out, sizeof(double) * 512 * 1024);
   hipMalloc(&clk, sizeof(unsigned long long) * 2 * 512);
-  // p = 32
-  run<32, 32, 2, 8, false>(256);  // current narrow geometry at p <= 32
-  run<64, 32, 2, 4, false>(256);  // 512-byte column segments
-  run<128, 32, 2, 2, false>(256); // 1 KiB column segments
-  run<32, 32, 2, 8, true>(256);
-  run<16, 32, 2, 8, false>(256);
-  run<16, 32, 4, 8, false>(256);
-  run<16, 32, 4, 8, true>(256);
-  run<32, 32, 3, 4, false>(256);
-  run<32, 32, 2, 4, false>(512);
-  run<16, 32, 3, 12, false>(256);
-  // p = 64
-  run<16, 64, 2, 8, false>(256);  // current narrow geometry at 32 < p <= 64
-  run<16, 64, 2, 8, true>(256);
-  run<8, 64, 4, 8, false>(256);
-  run<16, 64, 3, 4, false>(512);
-  run<32, 64, 2, 4, false>(256);
+  // the cache policy of the DMA (aux: 0 default, 2 non-temporal as the IRLS passes use, 1 glc,
+  // 3 glc + nt) on the narrow pass's two geometries
+  run<32, 32, 2, 8, false, 0>(256);
+  run<32, 32, 2, 8, false, 2>(256);
+  run<32, 32, 2, 8, false, 1>(256);
+  run<32, 32, 2, 8, false, 3>(256);
+  run<16, 64, 2, 8, false, 0>(256);
+  run<16, 64, 2, 8, false, 2>(256);
+  run<16, 64, 2, 8, false, 1>(256);
+  run<16, 64, 2, 8, false, 3>(256);
+  // depth / waves at nt
+  run<32, 32, 3, 4, false, 2>(256);
+  run<16, 32, 4, 8, false, 2>(256);
+  run<32, 32, 2, 4, false, 2>(512);
   return 0;
 }

@@ -511,13 +511,14 @@ CONFIG_STEPS = 3
 CONFIG_LM_FITS = 20
 
 
-def config_point(name: str, dev: int) -> dict:
+def config_point(name: str, dev: int, rows: int | None = None) -> dict:
     """One BASELINE config's per-GPU shard at N = 1 (the shapes and labels of WORKLOADS): time to
-    converge, ms per timed IRLS iteration (LM: per fit), rows/s and the roofline object."""
+    converge, ms per timed IRLS iteration (LM: per fit), rows/s and the roofline object.  `rows`
+    overrides the shard's rows (tests)."""
     import torch
     from sparkglm_amd import Engine
     wl = WORKLOADS[name]
-    n, p = wl["rows"], wl["p"]
+    n, p = rows or wl["rows"], wl["p"]
     eng = Engine(dev)
     try:
         t0 = time.perf_counter()

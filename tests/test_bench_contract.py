@@ -1,8 +1,11 @@
-"""bench.py's contract pieces that need no GPU: every workload maps to a BASELINE.json config
-with the family / shape it names, the traffic lookup, and the roofline bound choice."""
+"""bench.py's contract pieces: every workload maps to a BASELINE.json config with the family /
+shape it names, the traffic lookup, and the roofline bound choice (no GPU); the default run's
+config points on the device (gpu)."""
 import importlib.util
 import json
 import os
+
+import pytest
 
 from conftest import ROOT
 
@@ -267,3 +270,21 @@ def test_pass_roofline_from_stats():
     roof, _ = bench.pass_roofline(st, bench.WORKLOADS["poisson64"], 125_000_000, 64)
     assert roof["bound"] == "hbm" and roof["unit"] == "GB/s"
     assert "kernel_frac_of_pipe_bound" in roof["fp64_pipe"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,rows", [("lm20", 200_000), ("poisson64", 400_000), ("gamma2048", 20_000),
+                                       ("logit512", 100_000)])
+def test_config_point_runs_on_the_device(name, rows):
+    """The default bench run's configs_n1 points (bench.config_point) at reduced rows: each fits,
+    times its iterations and carries a roofline object with the bound SURVEY 8(d) assigns."""
+    r = bench.config_point(name, 0, rows=rows)
+    assert r["rows"] == rows and r["p"] == bench.WORKLOADS[name]["p"]
+    roof = r["roofline"]
+    assert roof["frac"] > 0 and roof["kernel_ms"] > 0
+    if name == "lm20":
+        assert r["ms_per_fit"] > 0 and roof["bound"] == "hbm"
+    else:
+        assert r["iters_to_converge"] >= 1 and r["ms_per_iter"] > 0
+        assert roof["bound"] == ("hbm" if name == "poisson64" else "mfma")
+        assert r["procedural_x"] == (name == "logit512")

@@ -240,3 +240,35 @@ def test_poisson_step_deviance_on_a_fresh_shard(eng):
     f = eng.fit_glm("poisson", "log")
     o = po.fit_glm(X, y, "poisson", "log", offset=off, prior=pr)
     assert f.iter == o.iter and rel(f.deviance, o.deviance) < 1e-12 and rel(f.dev_trace, o.dev_trace) < 1e-12
+
+
+@pytest.mark.parametrize("p", [5, 40, 100, 200, 300])
+def test_zero_prior_weights_drop_their_rows(eng, p):
+    """Prior weights with exact zeros (a-ext, R's glm(weights =)) on every pass path -- narrow
+    p <= 32 / <= 64, K1, K1r, wide: the fit matches the oracle, and equals the fit of the same data
+    with those rows removed (a zero weight zeroes the row's w, w z, deviance, Pearson and loglik
+    terms).  Not bitwise: the Gram sums in another row partition, and the start mu0 = mean(y) is
+    unweighted (GLM.scala:263), so the iterates differ on the way: the coefficients agree to
+    rounding, the standard errors -- taken from the Gram at the penultimate iterate, which the other
+    start moves -- to ~1e-9 (the oracle alike)."""
+    rng = np.random.default_rng(300 + p)
+    n = 9000 + 3 * p
+    X = rng.uniform(-1, 1, (n, p)) / np.sqrt(p)
+    X[:, 0] = 1.0
+    off = rng.uniform(-0.1, 0.1, n)
+    lam = np.exp(0.5 + X @ rng.normal(size=p) * 0.3 + off)
+    y = rng.poisson(lam).astype(float)
+    prior = rng.uniform(0.5, 1.5, n)
+    prior[rng.uniform(size=n) < 0.3] = 0.0
+    eng.set_data(X, y, offset=off, prior=prior)
+    f = eng.fit_glm("poisson", "log")
+    o = po.fit_glm(X, y, "poisson", "log", offset=off, prior=prior, nthreads=8)
+    assert f.iter == o.iter
+    assert rel(f.coefs, o.coefs) < TOL and rel(f.stderr, o.stderr) < TOL
+    assert rel([f.deviance, f.pearson, f.loglik], [o.deviance, o.pearson, o.loglik]) < TOL
+    keep = prior > 0
+    eng.set_data(X[keep], y[keep], offset=off[keep], prior=prior[keep])
+    g = eng.fit_glm("poisson", "log")
+    assert g.iter == f.iter
+    assert rel(g.coefs, f.coefs) < 1e-11 and rel(g.stderr, f.stderr) < 1e-7
+    assert rel([g.deviance, g.pearson, g.loglik], [f.deviance, f.pearson, f.loglik]) < 1e-11
